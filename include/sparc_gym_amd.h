@@ -1,0 +1,162 @@
+/* sparc_gym_amd.h — C ABI of the MI355X-native batched SPaRC step path.
+ *
+ * The reference (tobiTKM/SPaRC-Gym) is pure Python: one `SPaRC_Gym(gym.Env)` object holds one
+ * puzzle and `step(action)` runs on host numpy.  It has no FFI, so the entry points below are
+ * the C ABI its step path would bind through ctypes; each one cites the reference code it
+ * replaces (/root/reference/SPaRC_Gym/SPaRC_Gym.py).  The Python host layer in
+ * sparc-gym_amd/sparc_gym_amd/ (SPaRC_Gym, SPaRCVecEnv) binds exactly these symbols.
+ *
+ * Conventions
+ *  - Plain pointers and sizes; no torch / HIP types in the signatures (streams are void*).
+ *  - Every call returns SPARC_OK (0) or a negative error code; the message is available from
+ *    sparc_last_error(ctx) (or sparc_last_error(NULL) after a failed sparc_create).  No C++
+ *    exception crosses the ABI.
+ *  - `*_device` / rollout entry points take DEVICE pointers and are asynchronous on the
+ *    context's stream.  `*_host` entry points take host pointers and return after the data are
+ *    back on the host.
+ *  - One context per GPU, not reentrant; all work is ordered on its stream.
+ *
+ * Lattice encoding: planes are indexed [x, y] with x_size = 2*width+1, y_size = 2*height+1
+ * (SPaRC_Gym.py:243-248).  A point is bit b = x*pitch + y of a `words`-word bitboard, where
+ * pitch >= every puzzle's y_size and words*64 >= max x_size * pitch (words in {1, 2, 4}).
+ *
+ * Per-step outputs
+ *  reward code  int8  = normal_reward * 100: {-100, -1, 0, +1, +100}  (SPaRC_Gym.py:1201-1223);
+ *                       the host maps it back to the reference's Python values
+ *                       {-1 (int), -0.01, 0 (int), 0.01, 1 (int)}.
+ *  flags        uint8 bit0 terminated, bit1 truncated (SPaRC_Gym.py:1192-1199),
+ *                     bits2-5 legal actions after the step (info['legal_actions'], 1016),
+ *                     bit6 this step was an autoreset (gymnasium next-step mode).
+ *  outcome_reward (info['Rewards'], 1020) = done ? (code==-100 ? -1 : 1) : 0.
+ */
+#ifndef SPARC_GYM_AMD_H
+#define SPARC_GYM_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPARC_ABI_VERSION 1
+
+enum {
+    SPARC_OK = 0,
+    SPARC_E_INVALID = -1,   /* bad argument / shape / puzzle index              */
+    SPARC_E_HIP = -2,       /* HIP runtime error                                  */
+    SPARC_E_STATE = -3,     /* call order (e.g. step before load_puzzles/reset)   */
+    SPARC_E_NOMEM = -4
+};
+
+enum { SPARC_AUTORESET_NONE = 0, SPARC_AUTORESET_NEXT_STEP = 1 };
+
+enum {
+    SPARC_FLAG_TERMINATED = 1,
+    SPARC_FLAG_TRUNCATED = 2,
+    SPARC_FLAG_LEGAL_SHIFT = 2,
+    SPARC_FLAG_RESET = 64
+};
+
+/* Constructor kwargs of SPaRC_Gym.__init__ (SPaRC_Gym.py:46) that reach the step path, plus
+ * the batch shape.  The dataset kwargs (df_name/df_split/df_set) stay in the host layer. */
+typedef struct {
+    int32_t num_envs;
+    int32_t traceback;      /* SPaRC_Gym.py:65, 1041-1046, 1142-1166                      */
+    int32_t max_steps;      /* SPaRC_Gym.py:66, 1134                                      */
+    int32_t autoreset;      /* SPARC_AUTORESET_*; NONE reproduces the reference exactly   */
+    int32_t pitch;          /* bitboard row pitch (>= max y_size)                         */
+    int32_t words;          /* bitboard words: 1, 2 or 4                                  */
+    int64_t env_offset;     /* global id of env 0 (multi-GPU shards; random actions)      */
+} sparc_config;
+
+/* Static puzzle table, packed by the host loader (sparc_gym_amd/puzzles.py) from the
+ * processed puzzles of _process_puzzles (SPaRC_Gym.py:219-368).
+ *  open  [P][words]  bit set = lattice point inside the puzzle and gaps[x][y] == 0
+ *  info  [P][4]      w0 = x_size | y_size<<8 | start_x<<16 | start_y<<24
+ *                    w1 = target_x | target_y<<8 | flags<<16
+ *                         (flags bit0: solution_count > 0, bit1: some solution starts at start)
+ *                    w2 = global index of the puzzle's trie root, w3 = its trie node count
+ *  trie  [nodes][4]  solution-prefix trie, local (per puzzle) u16 indices, 0xFFFF = none:
+ *                    w0 = child[right] | child[up]<<16, w1 = child[left] | child[down]<<16,
+ *                    w2 = parent | terminal<<16, w3 = depth                                  */
+typedef struct {
+    int32_t num_puzzles;
+    int32_t num_nodes;
+    const uint64_t *open;
+    const uint32_t *info;
+    const uint32_t *trie;
+} sparc_puzzle_table;
+
+/* Host snapshot of the per-env state (any pointer may be NULL to skip that field). */
+typedef struct {
+    uint8_t *x, *y;         /* _agent_location              [N] */
+    uint16_t *path_len;     /* len(self.path)               [N] */
+    uint32_t *step;         /* current_step                 [N] */
+    uint32_t *puzzle;       /* current_puzzle_index         [N] */
+    int8_t *outcome;        /* outcome_reward               [N] */
+    uint8_t *pending;       /* done on the last step        [N] */
+    uint64_t *visited;      /* obs['base']['visited'] bits  [words][N] */
+} sparc_state_host;
+
+/* counter-based random action in {0,1,2,3} (splitmix64 finaliser of seed, env, t); stands in
+ * for env.action_space.sample() (Final_Product.py:29) in device rollouts. */
+static inline uint32_t sparc_rand_action(uint64_t seed, uint64_t env, uint64_t t) {
+    uint64_t z = seed + env * 0x9E3779B97F4A7C15ull + t * 0xD1B54A32D192ED03ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return (uint32_t)(z >> 62);
+}
+
+int sparc_abi_version(void);
+const char *sparc_last_error(const void *ctx);
+
+/* SPaRC_Gym.__init__ (SPaRC_Gym.py:46-90): allocate the SoA state for num_envs on `device`. */
+int sparc_create(int device, const sparc_config *cfg, void **ctx_out);
+int sparc_destroy(void *ctx);
+/* run on this HIP stream (hipStream_t as void*); NULL = the context's own stream */
+int sparc_set_stream(void *ctx, void *stream);
+int sparc_sync(void *ctx);
+
+/* _process_puzzles output -> device (SPaRC_Gym.py:88, 219-368); host arrays, copied. */
+int sparc_load_puzzles(void *ctx, const sparc_puzzle_table *table);
+
+/* reset / _load_puzzle (SPaRC_Gym.py:1057-1108, 141-187) for every env with mask[i] != 0
+ * (mask NULL = all) onto puzzle puzzle_index[i].  Arrays of length num_envs.  flags (may be
+ * NULL) receives, for the reset envs, the legal actions of the fresh state in bits 2-5 —
+ * info['legal_actions'] of reset()'s _get_info (SPaRC_Gym.py:1016, 1108). */
+int sparc_reset_host(void *ctx, const uint32_t *puzzle_index, const uint8_t *mask, uint8_t *flags);
+int sparc_reset_device(void *ctx, const uint32_t *d_puzzle_index, const uint8_t *d_mask, uint8_t *d_flags);
+
+/* step (SPaRC_Gym.py:1111-1238) for all envs: one action per env (values >= 4 are illegal
+ * and leave the agent in place, as `action in legal` fails at 1137). */
+int sparc_step_device(void *ctx, const uint8_t *d_actions, int8_t *d_reward, uint8_t *d_flags);
+int sparc_step_host(void *ctx, const uint8_t *actions, int8_t *reward, uint8_t *flags);
+
+/* T consecutive steps in ONE launch (state stays in registers): actions [T][N] device
+ * (or NULL: sparc_rand_action(seed, env_offset+i, t0+t)); reward/flags [T][N] device (may be
+ * NULL); stats [N][4] int32 device, accumulated: {sum of reward codes, done steps,
+ * solved (+1) steps, autoresets} (may be NULL).  Bit-identical to T sparc_step_device calls. */
+int sparc_rollout_device(void *ctx, int32_t T, const uint8_t *d_actions, uint64_t seed, uint64_t t0,
+                         int8_t *d_reward, uint8_t *d_flags, int32_t *d_stats);
+
+/* obs['base']['visited'] / obs['base']['agent_location'] as dense int32 planes
+ * [N][x_dim][y_dim] (x_dim >= max x_size, y_dim >= max y_size; device pointers, either may be
+ * NULL).  The reference returns these planes by reference every step (SPaRC_Gym.py:979). */
+int sparc_obs_pack_device(void *ctx, int32_t *d_visited, int32_t *d_agent, int32_t x_dim, int32_t y_dim);
+
+int sparc_read_state(void *ctx, const sparc_state_host *out);
+/* device-to-device copy of one SoA state array (`which` as in sparc_state_ptr) into d_out,
+ * ordered on the context's stream (e.g. the per-env puzzle index after autoresets). */
+int sparc_copy_state_device(void *ctx, int32_t which, void *d_out);
+
+/* device pointers of the context's SoA state (zero-copy views for the host layer):
+ * which: 0 visited [words][N] u64, 1 pos [N] u32 = x | y<<8 | len<<16 | off<<24,
+ *        2 aux [N] u32 = trie node | outcome<<16 (1: +1, 2: -1) | pending<<18,
+ *        3 step [N] u32, 4 puzzle [N] u32, 5 direction stack [2*words][N] u64 (traceback) */
+int sparc_state_ptr(void *ctx, int32_t which, void **d_ptr);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

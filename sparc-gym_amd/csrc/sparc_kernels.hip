@@ -1,0 +1,516 @@
+// sparc_kernels.hip — HIP kernels (gfx950) and the C ABI of include/sparc_gym_amd.h.
+//
+// Kernels (one lane per env, 256-lane workgroups, SoA state in HBM):
+//   k_reset    reset/_load_puzzle for masked envs                 (SPaRC_Gym.py:1057-1108)
+//   k_step     one step() per env, state HBM -> VGPR -> HBM        (SPaRC_Gym.py:1111-1238)
+//   k_rollout  T steps per launch with the state kept in VGPRs; actions [T][N] prefetched a
+//              chunk ahead, reward/flags streamed out per step     (the episode loop of
+//              Final_Product.py:26-38 / llm_host.py:182-242, batched)
+//   k_obs_pack dense int32 visited / agent_location planes         (_get_obs, SPaRC_Gym.py:979)
+// No MFMA: this is integer / bitboard work, bound by latency and HBM.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "sparc_env.hpp"
+#include "sparc_gym_amd.h"
+
+using namespace sparc;
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kChunk = 8;   // actions prefetched per lane in k_rollout
+
+template <int W, bool TB>
+__global__ void __launch_bounds__(kBlock) k_reset(Params p, const uint32_t* __restrict__ q,
+                                                  const uint8_t* __restrict__ mask, uint8_t* __restrict__ flg) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= p.n) return;
+    if (mask && !mask[i]) return;
+    const uint32_t pid = q[i];
+    if (pid >= p.tab.num_puzzles) {
+        atomicOr(p.err, 1);
+        return;
+    }
+    Env<W, TB> e;
+    e.reset(p, pid);
+    e.store(p, i);
+    if (flg) flg[i] = (uint8_t)(e.legal_mask(p.pitch) << 2);
+}
+
+template <int W, bool TB>
+__global__ void __launch_bounds__(kBlock) k_step(Params p, const uint8_t* __restrict__ act,
+                                                 int8_t* __restrict__ rew, uint8_t* __restrict__ flg) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= p.n) return;
+    Env<W, TB> e;
+    e.load(p, i);
+    uint32_t f;
+    const int c = e.advance(p, act[i], f);
+    e.store(p, i);
+    rew[i] = (int8_t)c;
+    flg[i] = (uint8_t)f;
+}
+
+template <int W, bool TB, bool RAND>
+__global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const uint8_t* __restrict__ act,
+                                                    uint64_t seed, uint64_t t0, int8_t* __restrict__ rew,
+                                                    uint8_t* __restrict__ flg, int4* __restrict__ stats) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= p.n) return;
+    Env<W, TB> e;
+    e.load(p, i);
+    const size_t n = p.n;
+    const uint64_t gid = p.env_offset + i;
+    int4 acc = make_int4(0, 0, 0, 0);
+    uint32_t cur[kChunk], nxt[kChunk];
+    if constexpr (!RAND) {
+#pragma unroll
+        for (int k = 0; k < kChunk; ++k) cur[k] = k < T ? act[(size_t)k * n + i] : 0u;
+    }
+    for (int32_t tc = 0; tc < T; tc += kChunk) {
+        if constexpr (!RAND) {   // prefetch the next chunk while this one is stepped
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k) {
+                const int32_t t = tc + kChunk + k;
+                nxt[k] = t < T ? act[(size_t)t * n + i] : 0u;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kChunk; ++k) {
+            const int32_t t = tc + k;
+            if (t < T) {
+                const uint32_t a = RAND ? uint_rand_action(seed, gid, t0 + (uint64_t)t) : cur[k];
+                uint32_t f;
+                const int c = e.advance(p, a, f);
+                if (rew) rew[(size_t)t * n + i] = (int8_t)c;
+                if (flg) flg[(size_t)t * n + i] = (uint8_t)f;
+                acc.x += c;
+                acc.y += (f & 3u) ? 1 : 0;
+                acc.z += ((f & 3u) && c == 100) ? 1 : 0;
+                acc.w += (f & 64u) ? 1 : 0;
+            }
+        }
+        if constexpr (!RAND) {
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k) cur[k] = nxt[k];
+        }
+    }
+    e.store(p, i);
+    if (stats) {
+        int4 s = stats[i];
+        s.x += acc.x;
+        s.y += acc.y;
+        s.z += acc.z;
+        s.w += acc.w;
+        stats[i] = s;
+    }
+}
+
+template <int W>
+__global__ void __launch_bounds__(kBlock) k_obs_pack(Params p, int32_t* __restrict__ vis_out,
+                                                     int32_t* __restrict__ agent_out, uint32_t xd, uint32_t yd) {
+    const size_t o = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const size_t per = (size_t)xd * yd;
+    if (o >= per * p.n) return;
+    const uint32_t i = (uint32_t)(o / per);
+    const uint32_t c = (uint32_t)(o - (size_t)i * per);
+    const uint32_t x = c / yd, y = c - x * yd;
+    const uint32_t ps = p.st.pos[i];
+    int32_t v = 0;
+    if (y < p.pitch) {
+        const uint32_t b = x * p.pitch + y;
+        if (b < 64u * W) v = (int32_t)((p.st.vis[(size_t)(b >> 6) * p.n + i] >> (b & 63)) & 1ull);
+    }
+    if (vis_out) vis_out[o] = v;
+    if (agent_out) agent_out[o] = (x == (ps & 0xFFu) && y == ((ps >> 8) & 0xFFu)) ? 1 : 0;
+}
+
+// ------------------------------------------------------------------------------ host side
+struct Ctx {
+    sparc_config cfg{};
+    int device = 0;
+    hipStream_t own = nullptr, stream = nullptr;
+    uint32_t n = 0;
+    int W = 1;
+    bool loaded = false, has_state = false;
+    uint32_t num_puzzles = 0, num_nodes = 0;
+    // device buffers
+    uint64_t *vis = nullptr, *dirs = nullptr;
+    uint32_t *pos = nullptr, *aux = nullptr, *step = nullptr, *pid = nullptr;
+    uint64_t* t_open = nullptr;
+    uint4 *t_info = nullptr, *t_trie = nullptr;
+    int32_t* err = nullptr;
+    uint8_t *s_act = nullptr, *s_flags = nullptr, *s_mask = nullptr;
+    int8_t* s_rew = nullptr;
+    uint32_t* s_pidx = nullptr;
+    std::string msg;
+};
+
+thread_local std::string g_err;
+
+int fail(Ctx* c, int code, const std::string& m) {
+    if (c) c->msg = m;
+    g_err = m;
+    return code;
+}
+
+#define HIPCHK(c, expr)                                                              \
+    do {                                                                             \
+        hipError_t _e = (expr);                                                      \
+        if (_e != hipSuccess)                                                        \
+            return fail((c), SPARC_E_HIP, std::string(#expr ": ") + hipGetErrorString(_e)); \
+    } while (0)
+
+Params make_params(const Ctx* c) {
+    Params p{};
+    p.tab.open = c->t_open;
+    p.tab.info = c->t_info;
+    p.tab.trie = c->t_trie;
+    p.tab.num_puzzles = c->num_puzzles;
+    p.st.vis = c->vis;
+    p.st.dirs = c->dirs;
+    p.st.pos = c->pos;
+    p.st.aux = c->aux;
+    p.st.step = c->step;
+    p.st.pid = c->pid;
+    p.n = c->n;
+    p.pitch = (uint32_t)c->cfg.pitch;
+    p.max_steps = c->cfg.max_steps;
+    p.autoreset = c->cfg.autoreset;
+    p.env_offset = (uint64_t)c->cfg.env_offset;
+    p.err = c->err;
+    return p;
+}
+
+inline dim3 grid_for(size_t n) { return dim3((unsigned)((n + kBlock - 1) / kBlock)); }
+
+// call f(integral_constant<W>, bool_constant<TB>) for the runtime (W, TB)
+template <class F>
+void dispatch_w_tb(int w, bool tb, F&& f) {
+    using T1 = std::integral_constant<int, 1>;
+    using T2 = std::integral_constant<int, 2>;
+    using T4 = std::integral_constant<int, 4>;
+    if (w == 1) tb ? f(T1{}, std::true_type{}) : f(T1{}, std::false_type{});
+    else if (w == 2) tb ? f(T2{}, std::true_type{}) : f(T2{}, std::false_type{});
+    else tb ? f(T4{}, std::true_type{}) : f(T4{}, std::false_type{});
+}
+
+int check_ctx(Ctx* c, bool need_state) {
+    if (!c) return fail(nullptr, SPARC_E_INVALID, "null context");
+    if (!c->loaded) return fail(c, SPARC_E_STATE, "sparc_load_puzzles has not been called");
+    if (need_state && !c->has_state) return fail(c, SPARC_E_STATE, "sparc_reset has not been called");
+    HIPCHK(c, hipSetDevice(c->device));
+    return SPARC_OK;
+}
+
+int launch_check(Ctx* c) {
+    HIPCHK(c, hipGetLastError());
+    return SPARC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sparc_abi_version(void) { return SPARC_ABI_VERSION; }
+
+const char* sparc_last_error(const void* ctx) {
+    return ctx ? static_cast<const Ctx*>(ctx)->msg.c_str() : g_err.c_str();
+}
+
+int sparc_create(int device, const sparc_config* cfg, void** ctx_out) {
+    if (!cfg || !ctx_out) return fail(nullptr, SPARC_E_INVALID, "null argument");
+    *ctx_out = nullptr;
+    if (cfg->num_envs < 1) return fail(nullptr, SPARC_E_INVALID, "num_envs must be >= 1");
+    if (cfg->words != 1 && cfg->words != 2 && cfg->words != 4)
+        return fail(nullptr, SPARC_E_INVALID, "words must be 1, 2 or 4");
+    if (cfg->pitch < 1 || cfg->pitch > 255) return fail(nullptr, SPARC_E_INVALID, "pitch must be in 1..255");
+    if (cfg->traceback != 0 && cfg->traceback != 1) return fail(nullptr, SPARC_E_INVALID, "traceback must be 0/1");
+    if (cfg->autoreset != SPARC_AUTORESET_NONE && cfg->autoreset != SPARC_AUTORESET_NEXT_STEP)
+        return fail(nullptr, SPARC_E_INVALID, "unknown autoreset mode");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(nullptr, SPARC_E_HIP, "no HIP device available");
+    if (device < 0 || device >= ndev) return fail(nullptr, SPARC_E_INVALID, "bad device ordinal");
+    Ctx* c = new Ctx();
+    c->cfg = *cfg;
+    c->device = device;
+    c->n = (uint32_t)cfg->num_envs;
+    c->W = cfg->words;
+    const size_t n = c->n;
+    auto cleanup = [&](int code) {
+        sparc_destroy(c);
+        return code;
+    };
+    if (hipSetDevice(device) != hipSuccess) return cleanup(fail(nullptr, SPARC_E_HIP, "hipSetDevice failed"));
+    if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess)
+        return cleanup(fail(nullptr, SPARC_E_HIP, "hipStreamCreate failed"));
+    c->stream = c->own;
+    bool ok = hipMalloc(&c->vis, sizeof(uint64_t) * n * c->W) == hipSuccess &&
+              hipMalloc(&c->pos, sizeof(uint32_t) * n) == hipSuccess &&
+              hipMalloc(&c->aux, sizeof(uint32_t) * n) == hipSuccess &&
+              hipMalloc(&c->step, sizeof(uint32_t) * n) == hipSuccess &&
+              hipMalloc(&c->pid, sizeof(uint32_t) * n) == hipSuccess &&
+              hipMalloc(&c->err, sizeof(int32_t)) == hipSuccess &&
+              hipMalloc(&c->s_act, n) == hipSuccess && hipMalloc(&c->s_flags, n) == hipSuccess &&
+              hipMalloc(&c->s_mask, n) == hipSuccess && hipMalloc(&c->s_rew, n) == hipSuccess &&
+              hipMalloc(&c->s_pidx, sizeof(uint32_t) * n) == hipSuccess;
+    if (ok && cfg->traceback) ok = hipMalloc(&c->dirs, sizeof(uint64_t) * n * 2 * c->W) == hipSuccess;
+    if (!ok) return cleanup(fail(nullptr, SPARC_E_NOMEM, "hipMalloc failed for the env state"));
+    if (hipMemset(c->err, 0, sizeof(int32_t)) != hipSuccess)
+        return cleanup(fail(nullptr, SPARC_E_HIP, "hipMemset failed"));
+    *ctx_out = c;
+    return SPARC_OK;
+}
+
+int sparc_destroy(void* ctx) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c) return SPARC_OK;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    void* bufs[] = {c->vis, c->dirs, c->pos, c->aux, c->step, c->pid, c->t_open, c->t_info, c->t_trie,
+                    c->err, c->s_act, c->s_flags, c->s_mask, c->s_rew, c->s_pidx};
+    for (void* b : bufs)
+        if (b) (void)hipFree(b);
+    if (c->own) (void)hipStreamDestroy(c->own);
+    delete c;
+    return SPARC_OK;
+}
+
+int sparc_set_stream(void* ctx, void* stream) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c) return fail(nullptr, SPARC_E_INVALID, "null context");
+    c->stream = stream ? static_cast<hipStream_t>(stream) : c->own;
+    return SPARC_OK;
+}
+
+int sparc_sync(void* ctx) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c) return fail(nullptr, SPARC_E_INVALID, "null context");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    int32_t e = 0;
+    HIPCHK(c, hipMemcpy(&e, c->err, sizeof(e), hipMemcpyDeviceToHost));
+    if (e) {
+        HIPCHK(c, hipMemset(c->err, 0, sizeof(int32_t)));
+        return fail(c, SPARC_E_INVALID, "device-side puzzle index out of range in a reset");
+    }
+    return SPARC_OK;
+}
+
+int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c || !t || !t->open || !t->info) return fail(c, SPARC_E_INVALID, "null argument");
+    if (t->num_puzzles < 1) return fail(c, SPARC_E_INVALID, "empty puzzle table");
+    if (t->num_nodes < 0 || (t->num_nodes > 0 && !t->trie)) return fail(c, SPARC_E_INVALID, "bad trie");
+    const int W = c->W;
+    const uint32_t pitch = (uint32_t)c->cfg.pitch;
+    // validate every index the kernels will follow, so no launch can read out of bounds
+    for (int q = 0; q < t->num_puzzles; ++q) {
+        const uint32_t* inf = t->info + 4 * (size_t)q;
+        const uint32_t X = inf[0] & 0xFF, Y = (inf[0] >> 8) & 0xFF;
+        const uint32_t sx = (inf[0] >> 16) & 0xFF, sy = inf[0] >> 24;
+        const uint32_t tx = inf[1] & 0xFF, ty = (inf[1] >> 8) & 0xFF, fl = inf[1] >> 16;
+        const uint32_t base = inf[2], cnt = inf[3];
+        char m[160];
+        if (X < 1 || Y < 1 || Y > pitch || (X - 1) * pitch + Y > 64u * W) {
+            snprintf(m, sizeof m, "puzzle %d: lattice %ux%u does not fit pitch %u / %d words", q, X, Y, pitch, W);
+            return fail(c, SPARC_E_INVALID, m);
+        }
+        if (sx >= X || sy >= Y || tx >= X || ty >= Y) {
+            snprintf(m, sizeof m, "puzzle %d: start/target outside the lattice", q);
+            return fail(c, SPARC_E_INVALID, m);
+        }
+        if ((fl & 2u) && (cnt == 0 || (uint64_t)base + cnt > (uint64_t)t->num_nodes || cnt > 0xFFFF)) {
+            snprintf(m, sizeof m, "puzzle %d: trie range out of bounds", q);
+            return fail(c, SPARC_E_INVALID, m);
+        }
+        if (fl & 2u) {
+            for (uint32_t k = 0; k < cnt; ++k) {
+                const uint32_t* r = t->trie + 4 * ((size_t)base + k);
+                const uint32_t ch[4] = {r[0] & 0xFFFF, r[0] >> 16, r[1] & 0xFFFF, r[1] >> 16};
+                for (uint32_t v : ch)
+                    if (v != kNone && v >= cnt) return fail(c, SPARC_E_INVALID, "trie child out of range");
+                const uint32_t par = r[2] & 0xFFFF;
+                if (k > 0 && par >= cnt) return fail(c, SPARC_E_INVALID, "trie parent out of range");
+            }
+        }
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->t_open) HIPCHK(c, hipFree(c->t_open));
+    if (c->t_info) HIPCHK(c, hipFree(c->t_info));
+    if (c->t_trie) HIPCHK(c, hipFree(c->t_trie));
+    c->t_open = nullptr;
+    c->t_info = nullptr;
+    c->t_trie = nullptr;
+    const size_t P = (size_t)t->num_puzzles, nn = (size_t)(t->num_nodes > 0 ? t->num_nodes : 1);
+    HIPCHK(c, hipMalloc(&c->t_open, sizeof(uint64_t) * P * W));
+    HIPCHK(c, hipMalloc(&c->t_info, sizeof(uint4) * P));
+    HIPCHK(c, hipMalloc(&c->t_trie, sizeof(uint4) * nn));
+    HIPCHK(c, hipMemcpy(c->t_open, t->open, sizeof(uint64_t) * P * W, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->t_info, t->info, sizeof(uint4) * P, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemset(c->t_trie, 0xFF, sizeof(uint4) * nn));
+    if (t->num_nodes > 0)
+        HIPCHK(c, hipMemcpy(c->t_trie, t->trie, sizeof(uint4) * (size_t)t->num_nodes, hipMemcpyHostToDevice));
+    c->num_puzzles = (uint32_t)t->num_puzzles;
+    c->num_nodes = (uint32_t)t->num_nodes;
+    c->loaded = true;
+    c->has_state = false;   // old state may point at puzzles that no longer exist
+    return SPARC_OK;
+}
+
+int sparc_reset_device(void* ctx, const uint32_t* d_q, const uint8_t* d_mask, uint8_t* d_flags) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    int rc = check_ctx(c, false);
+    if (rc) return rc;
+    if (!d_q) return fail(c, SPARC_E_INVALID, "null puzzle_index");
+    if (d_mask && !c->has_state) return fail(c, SPARC_E_STATE, "first reset must cover every env (mask NULL)");
+    const Params p = make_params(c);
+    dispatch_w_tb(c->W, c->cfg.traceback, [&](auto w, auto tb) {
+        k_reset<decltype(w)::value, decltype(tb)::value><<<grid_for(c->n), kBlock, 0, c->stream>>>(p, d_q, d_mask, d_flags);
+    });
+    rc = launch_check(c);
+    if (rc) return rc;
+    c->has_state = true;
+    return SPARC_OK;
+}
+
+int sparc_reset_host(void* ctx, const uint32_t* q, const uint8_t* mask, uint8_t* flags) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    int rc = check_ctx(c, false);
+    if (rc) return rc;
+    if (!q) return fail(c, SPARC_E_INVALID, "null puzzle_index");
+    for (uint32_t i = 0; i < c->n; ++i)
+        if ((!mask || mask[i]) && q[i] >= c->num_puzzles) return fail(c, SPARC_E_INVALID, "puzzle index out of range");
+    HIPCHK(c, hipMemcpyAsync(c->s_pidx, q, sizeof(uint32_t) * c->n, hipMemcpyHostToDevice, c->stream));
+    if (mask) HIPCHK(c, hipMemcpyAsync(c->s_mask, mask, c->n, hipMemcpyHostToDevice, c->stream));
+    rc = sparc_reset_device(c, c->s_pidx, mask ? c->s_mask : nullptr, flags ? c->s_flags : nullptr);
+    if (rc) return rc;
+    if (flags) HIPCHK(c, hipMemcpyAsync(flags, c->s_flags, c->n, hipMemcpyDeviceToHost, c->stream));
+    return sparc_sync(c);
+}
+
+int sparc_step_device(void* ctx, const uint8_t* d_act, int8_t* d_rew, uint8_t* d_flags) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    int rc = check_ctx(c, true);
+    if (rc) return rc;
+    if (!d_act || !d_rew || !d_flags) return fail(c, SPARC_E_INVALID, "null argument");
+    const Params p = make_params(c);
+    dispatch_w_tb(c->W, c->cfg.traceback, [&](auto w, auto tb) {
+        k_step<decltype(w)::value, decltype(tb)::value><<<grid_for(c->n), kBlock, 0, c->stream>>>(p, d_act, d_rew,
+                                                                                                  d_flags);
+    });
+    return launch_check(c);
+}
+
+int sparc_step_host(void* ctx, const uint8_t* act, int8_t* rew, uint8_t* flags) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    int rc = check_ctx(c, true);
+    if (rc) return rc;
+    if (!act || !rew || !flags) return fail(c, SPARC_E_INVALID, "null argument");
+    HIPCHK(c, hipMemcpyAsync(c->s_act, act, c->n, hipMemcpyHostToDevice, c->stream));
+    rc = sparc_step_device(c, c->s_act, c->s_rew, c->s_flags);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(rew, c->s_rew, c->n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(flags, c->s_flags, c->n, hipMemcpyDeviceToHost, c->stream));
+    return sparc_sync(c);
+}
+
+int sparc_rollout_device(void* ctx, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_t t0, int8_t* d_rew,
+                         uint8_t* d_flags, int32_t* d_stats) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    int rc = check_ctx(c, true);
+    if (rc) return rc;
+    if (T < 0) return fail(c, SPARC_E_INVALID, "T must be >= 0");
+    if (T == 0) return SPARC_OK;
+    if ((uint64_t)T * c->n > (1ull << 40)) return fail(c, SPARC_E_INVALID, "T*N too large");
+    const Params p = make_params(c);
+    int4* st = reinterpret_cast<int4*>(d_stats);
+    dispatch_w_tb(c->W, c->cfg.traceback, [&](auto w, auto tb) {
+        constexpr int W = decltype(w)::value;
+        constexpr bool TB = decltype(tb)::value;
+        if (d_act)
+            k_rollout<W, TB, false><<<grid_for(c->n), kBlock, 0, c->stream>>>(p, T, d_act, seed, t0, d_rew, d_flags, st);
+        else
+            k_rollout<W, TB, true><<<grid_for(c->n), kBlock, 0, c->stream>>>(p, T, nullptr, seed, t0, d_rew, d_flags, st);
+    });
+    return launch_check(c);
+}
+
+int sparc_obs_pack_device(void* ctx, int32_t* d_vis, int32_t* d_agent, int32_t xd, int32_t yd) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    int rc = check_ctx(c, true);
+    if (rc) return rc;
+    if (xd < 1 || yd < 1 || xd > 255 || yd > 255) return fail(c, SPARC_E_INVALID, "bad plane dims");
+    const Params p = make_params(c);
+    const size_t total = (size_t)c->n * xd * yd;
+    const dim3 g = grid_for(total);
+    if (c->W == 1) k_obs_pack<1><<<g, kBlock, 0, c->stream>>>(p, d_vis, d_agent, xd, yd);
+    else if (c->W == 2) k_obs_pack<2><<<g, kBlock, 0, c->stream>>>(p, d_vis, d_agent, xd, yd);
+    else k_obs_pack<4><<<g, kBlock, 0, c->stream>>>(p, d_vis, d_agent, xd, yd);
+    return launch_check(c);
+}
+
+int sparc_read_state(void* ctx, const sparc_state_host* o) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    int rc = check_ctx(c, true);
+    if (rc) return rc;
+    if (!o) return fail(c, SPARC_E_INVALID, "null argument");
+    const size_t n = c->n;
+    std::vector<uint32_t> pos(n), aux(n);
+    HIPCHK(c, hipMemcpyAsync(pos.data(), c->pos, 4 * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(aux.data(), c->aux, 4 * n, hipMemcpyDeviceToHost, c->stream));
+    if (o->step) HIPCHK(c, hipMemcpyAsync(o->step, c->step, 4 * n, hipMemcpyDeviceToHost, c->stream));
+    if (o->puzzle) HIPCHK(c, hipMemcpyAsync(o->puzzle, c->pid, 4 * n, hipMemcpyDeviceToHost, c->stream));
+    if (o->visited)
+        HIPCHK(c, hipMemcpyAsync(o->visited, c->vis, 8 * n * c->W, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (size_t i = 0; i < n; ++i) {
+        if (o->x) o->x[i] = (uint8_t)(pos[i] & 0xFF);
+        if (o->y) o->y[i] = (uint8_t)((pos[i] >> 8) & 0xFF);
+        if (o->path_len) o->path_len[i] = (uint16_t)((pos[i] >> 16) & 0xFF);
+        const uint32_t oc = (aux[i] >> 16) & 3u;
+        if (o->outcome) o->outcome[i] = (int8_t)(oc == 1 ? 1 : (oc == 2 ? -1 : 0));
+        if (o->pending) o->pending[i] = (uint8_t)((aux[i] >> 18) & 1u);
+    }
+    return SPARC_OK;
+}
+
+int sparc_state_ptr(void* ctx, int32_t which, void** d_ptr) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c || !d_ptr) return fail(c, SPARC_E_INVALID, "null argument");
+    switch (which) {
+        case 0: *d_ptr = c->vis; break;
+        case 1: *d_ptr = c->pos; break;
+        case 2: *d_ptr = c->aux; break;
+        case 3: *d_ptr = c->step; break;
+        case 4: *d_ptr = c->pid; break;
+        case 5: *d_ptr = c->dirs; break;
+        default: return fail(c, SPARC_E_INVALID, "unknown state field");
+    }
+    return SPARC_OK;
+}
+
+int sparc_copy_state_device(void* ctx, int32_t which, void* d_out) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    int rc = check_ctx(c, true);
+    if (rc) return rc;
+    if (!d_out) return fail(c, SPARC_E_INVALID, "null argument");
+    void* src = nullptr;
+    rc = sparc_state_ptr(c, which, &src);
+    if (rc) return rc;
+    if (!src) return fail(c, SPARC_E_INVALID, "state field not allocated (traceback off)");
+    const size_t n = c->n;
+    const size_t bytes = which == 0 ? 8 * n * c->W : which == 5 ? 16 * n * c->W : 4 * n;
+    HIPCHK(c, hipMemcpyAsync(d_out, src, bytes, hipMemcpyDeviceToDevice, c->stream));
+    return SPARC_OK;
+}
+
+}  // extern "C"

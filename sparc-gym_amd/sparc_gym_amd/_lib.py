@@ -1,0 +1,88 @@
+"""ctypes binding of include/sparc_gym_amd.h (libsparc_gym_amd.so, built for gfx950).
+
+There is no fallback: if the HIP library is missing or fails to load, importing the env
+classes raises.  Build it with ``make -C sparc-gym_amd`` (or ``__graft_entry__.build()``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsparc_gym_amd.so")
+
+SPARC_OK = 0
+AUTORESET = {"none": 0, "next_step": 1}
+
+c_void_p, c_int32, c_uint64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint64
+
+
+class SparcConfig(ctypes.Structure):
+    _fields_ = [("num_envs", ctypes.c_int32), ("traceback", ctypes.c_int32), ("max_steps", ctypes.c_int32),
+                ("autoreset", ctypes.c_int32), ("pitch", ctypes.c_int32), ("words", ctypes.c_int32),
+                ("env_offset", ctypes.c_int64)]
+
+
+class SparcPuzzleTable(ctypes.Structure):
+    _fields_ = [("num_puzzles", ctypes.c_int32), ("num_nodes", ctypes.c_int32),
+                ("open", c_void_p), ("info", c_void_p), ("trie", c_void_p)]
+
+
+class SparcStateHost(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("y", c_void_p), ("path_len", c_void_p), ("step", c_void_p),
+                ("puzzle", c_void_p), ("outcome", c_void_p), ("pending", c_void_p), ("visited", c_void_p)]
+
+
+_SIGS = {
+    "sparc_abi_version": ([], c_int32),
+    "sparc_last_error": ([c_void_p], ctypes.c_char_p),
+    "sparc_create": ([ctypes.c_int, ctypes.POINTER(SparcConfig), ctypes.POINTER(c_void_p)], c_int32),
+    "sparc_destroy": ([c_void_p], c_int32),
+    "sparc_set_stream": ([c_void_p, c_void_p], c_int32),
+    "sparc_sync": ([c_void_p], c_int32),
+    "sparc_load_puzzles": ([c_void_p, ctypes.POINTER(SparcPuzzleTable)], c_int32),
+    "sparc_reset_host": ([c_void_p, c_void_p, c_void_p, c_void_p], c_int32),
+    "sparc_reset_device": ([c_void_p, c_void_p, c_void_p, c_void_p], c_int32),
+    "sparc_step_device": ([c_void_p, c_void_p, c_void_p, c_void_p], c_int32),
+    "sparc_step_host": ([c_void_p, c_void_p, c_void_p, c_void_p], c_int32),
+    "sparc_rollout_device": ([c_void_p, c_int32, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p],
+                             c_int32),
+    "sparc_obs_pack_device": ([c_void_p, c_void_p, c_void_p, c_int32, c_int32], c_int32),
+    "sparc_read_state": ([c_void_p, ctypes.POINTER(SparcStateHost)], c_int32),
+    "sparc_state_ptr": ([c_void_p, c_int32, ctypes.POINTER(c_void_p)], c_int32),
+    "sparc_copy_state_device": ([c_void_p, c_int32, c_void_p], c_int32),
+}
+EXPORTS = tuple(_SIGS)
+
+_lib = None
+
+
+class SparcError(RuntimeError):
+    pass
+
+
+def load(path=LIB_PATH):
+    """Load and type the HIP library (cached).  Raises if it is missing: no CPU fallback."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(f"{path} not found: build the HIP extension (make -C sparc-gym_amd)")
+    lib = ctypes.CDLL(path)
+    for name, (args, res) in _SIGS.items():
+        f = getattr(lib, name)
+        f.argtypes = args
+        f.restype = res
+    if lib.sparc_abi_version() != 1:
+        raise ImportError("libsparc_gym_amd ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def check(rc, ctx=None):
+    if rc != SPARC_OK:
+        msg = load().sparc_last_error(ctx)
+        msg = msg.decode() if msg else "unknown error"
+        if rc == -1:
+            raise ValueError(msg)
+        raise SparcError(f"sparc error {rc}: {msg}")

@@ -1,0 +1,131 @@
+"""SparcCore: owns one C-ABI context (one GPU, one batch of envs) and its calls.
+
+Thin, typed wrapper over include/sparc_gym_amd.h used by SPaRCVecEnv (batched) and SPaRC_Gym
+(batch of one).  Device pointers are plain ints (e.g. torch ``tensor.data_ptr()``).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .puzzles import PuzzleTable
+
+INT32_MAX = 2**31 - 1
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+class SparcCore:
+    def __init__(self, table: PuzzleTable, num_envs: int, traceback=False, max_steps=2000,
+                 autoreset="none", device=0, env_offset=0):
+        self.lib = _lib.load()
+        if autoreset not in _lib.AUTORESET:
+            raise ValueError(f"autoreset must be one of {sorted(_lib.AUTORESET)}")
+        self.table = table
+        self.num_envs = int(num_envs)
+        self.traceback = bool(traceback)
+        self.max_steps = int(max(min(int(max_steps), INT32_MAX), -INT32_MAX - 1))
+        self.device = int(device)
+        cfg = _lib.SparcConfig(self.num_envs, int(self.traceback), self.max_steps, _lib.AUTORESET[autoreset],
+                               table.pitch, table.words, int(env_offset))
+        ctx = ctypes.c_void_p()
+        _lib.check(self.lib.sparc_create(self.device, ctypes.byref(cfg), ctypes.byref(ctx)))
+        self.ctx = ctx
+        self.load_table(table)
+
+    # ---------------------------------------------------------------- lifecycle
+    def load_table(self, table: PuzzleTable):
+        open_ = np.ascontiguousarray(table.open, np.uint64)
+        info = np.ascontiguousarray(table.info, np.uint32)
+        trie = np.ascontiguousarray(table.trie, np.uint32)
+        t = _lib.SparcPuzzleTable(len(info), len(trie), open_.ctypes.data, info.ctypes.data,
+                                  trie.ctypes.data if len(trie) else None)
+        self._check(self.lib.sparc_load_puzzles(self.ctx, ctypes.byref(t)))
+        self.table = table
+
+    def close(self):
+        if getattr(self, "ctx", None) is not None and self.ctx.value:
+            self.lib.sparc_destroy(self.ctx)
+        self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    def _check(self, rc):
+        _lib.check(rc, self.ctx)
+
+    def set_stream(self, stream_handle):
+        self._check(self.lib.sparc_set_stream(self.ctx, stream_handle or None))
+
+    def sync(self):
+        self._check(self.lib.sparc_sync(self.ctx))
+
+    # ---------------------------------------------------------------- host-pointer calls
+    def reset_host(self, puzzle_index, mask=None):
+        q = np.ascontiguousarray(puzzle_index, np.uint32)
+        if q.shape != (self.num_envs,):
+            raise ValueError(f"puzzle_index must have shape ({self.num_envs},)")
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+        if m is not None and m.shape != (self.num_envs,):
+            raise ValueError("mask shape mismatch")
+        flags = np.zeros(self.num_envs, np.uint8)
+        self._check(self.lib.sparc_reset_host(self.ctx, _ptr(q), _ptr(m), _ptr(flags)))
+        return flags
+
+    def step_host(self, actions):
+        a = np.ascontiguousarray(actions, np.uint8)
+        if a.shape != (self.num_envs,):
+            raise ValueError(f"actions must have shape ({self.num_envs},)")
+        rew = np.empty(self.num_envs, np.int8)
+        flags = np.empty(self.num_envs, np.uint8)
+        self._check(self.lib.sparc_step_host(self.ctx, _ptr(a), _ptr(rew), _ptr(flags)))
+        return rew, flags
+
+    def read_state(self):
+        n, W = self.num_envs, self.table.words
+        out = {"x": np.empty(n, np.uint8), "y": np.empty(n, np.uint8), "path_len": np.empty(n, np.uint16),
+               "step": np.empty(n, np.uint32), "puzzle": np.empty(n, np.uint32), "outcome": np.empty(n, np.int8),
+               "pending": np.empty(n, np.uint8), "visited": np.empty((W, n), np.uint64)}
+        s = _lib.SparcStateHost(*(out[k].ctypes.data for k in
+                                  ("x", "y", "path_len", "step", "puzzle", "outcome", "pending", "visited")))
+        self._check(self.lib.sparc_read_state(self.ctx, ctypes.byref(s)))
+        return out
+
+    # ---------------------------------------------------------------- device-pointer calls (async)
+    def reset_device(self, d_puzzle_index, d_mask=None, d_flags=None):
+        self._check(self.lib.sparc_reset_device(self.ctx, d_puzzle_index, d_mask, d_flags))
+
+    def step_device(self, d_actions, d_reward, d_flags):
+        self._check(self.lib.sparc_step_device(self.ctx, d_actions, d_reward, d_flags))
+
+    def rollout_device(self, T, d_actions, d_reward, d_flags, d_stats=None, seed=0, t0=0):
+        self._check(self.lib.sparc_rollout_device(self.ctx, int(T), d_actions, int(seed) & (2**64 - 1),
+                                                  int(t0), d_reward, d_flags, d_stats))
+
+    def copy_state_device(self, which, d_out):
+        self._check(self.lib.sparc_copy_state_device(self.ctx, int(which), d_out))
+
+    def obs_pack_device(self, d_visited, d_agent, x_dim, y_dim):
+        self._check(self.lib.sparc_obs_pack_device(self.ctx, d_visited, d_agent, int(x_dim), int(y_dim)))
+
+
+def visited_planes(bits, table: PuzzleTable, x_dim=None, y_dim=None):
+    """Decode visited bitboards [words][N] into int32 planes [N][x_dim][y_dim] (host)."""
+    W, n = bits.shape
+    x_dim = table.x_max if x_dim is None else x_dim
+    y_dim = table.y_max if y_dim is None else y_dim
+    xs, ys = np.meshgrid(np.arange(x_dim), np.arange(y_dim), indexing="ij")
+    b = xs * table.pitch + ys
+    valid = (ys < table.pitch) & (b < 64 * W)
+    b = np.where(valid, b, 0)
+    words = bits[(b >> 6), :]                                   # [x, y, N]
+    v = (words >> (b & 63).astype(np.uint64)[..., None]) & np.uint64(1)
+    v = np.where(valid[..., None], v, 0).astype(np.int32)
+    return np.ascontiguousarray(np.moveaxis(v, -1, 0))

@@ -1,0 +1,221 @@
+"""SPaRC_Gym: drop-in for the reference's single-puzzle ``gymnasium.Env``.
+
+Same constructor kwargs, ``reset/step/render/close``, ``Discrete(4)`` actions, ``'new'`` dict
+and ``'SPaRC'`` text observations, and the same ``info`` keys as
+/root/reference/SPaRC_Gym/SPaRC_Gym.py (class at 44-1315).  The step itself runs on the GPU
+through the C ABI (a batch of one env); host code only mirrors the observation planes from
+the device state.
+
+Differences (documented in DESIGN.md):
+* ``puzzles=`` accepts a local DataFrame / list of records in the SPaRC schema, because the
+  hub dataset (``load_dataset``, SPaRC_Gym.py:77) needs the network; ``df_name`` etc. are
+  still honoured when ``puzzles`` is None.
+* Every reset restores pristine planes (the reference's first load of a puzzle); the reference
+  aliases the planes across re-loads (SPaRC_Gym.py:149-151).
+* ``info['rule_status']`` (the info-only rule audit, 941-950) is ``{}``: out of scope.
+* ``render_mode='human'/'llm'`` needs pygame, which is not available: raises.
+"""
+from __future__ import annotations
+
+import json
+from collections import OrderedDict
+
+import numpy as np
+
+from .core import SparcCore
+from .puzzles import pack_table, process_puzzles
+from .spaces import Box, Dict, Discrete, Env, Text
+
+_REWARD = {0: 0, 1: 0.01, -1: -0.01, 100: 1, -100: -1}   # code -> the reference's Python value
+
+
+def reward_value(code):
+    """int8 reward code -> the reference's value and type (SPaRC_Gym.py:1133, 1207-1223)."""
+    return _REWARD[int(code)]
+
+
+def action_code(action):
+    """Map a caller's action to 0..3, or 255 if `action in legal_actions` can never hold."""
+    for k in range(4):
+        try:
+            if action == k:
+                return k
+        except Exception:  # noqa: BLE001
+            return 255
+    return 255
+
+
+def load_puzzle_source(puzzles, df_name, df_split, df_set):
+    if puzzles is not None:
+        return puzzles
+    from datasets import load_dataset   # SPaRC_Gym.py:77-78 (network on first use)
+    return load_dataset(df_name, df_split, split=df_set).to_pandas()
+
+
+class SPaRC_Gym(Env):
+    metadata = {"render_modes": ["human", "llm"], "render_fps": 30}
+
+    def __init__(self, df_name="lkaesberg/SPaRC", df_split="all", df_set="test", render_mode=None,
+                 observation="new", traceback=False, max_steps=2000, puzzles=None, device=0):
+        self.render_mode = render_mode
+        self.observation = observation
+        self.traceback = traceback
+        self.max_steps = max_steps
+        if render_mode in ("human", "llm"):
+            raise NotImplementedError("pygame renderers are not part of this build (render_mode must be None)")
+        df = load_puzzle_source(puzzles, df_name, df_split, df_set)
+        self.current_puzzle_index = 0
+        self.current_step = 0
+        self.rule_status = {}
+        if df is None or isinstance(df, Exception):
+            raise ValueError("No valid dataframe provided")                          # 86-87
+        self.puzzles = process_puzzles(df, observation)
+        self._core = SparcCore(pack_table(self.puzzles), 1, traceback, max_steps, "none", device)
+        self._legal = 0
+        self._load_puzzle(self.current_puzzle_index)
+
+    # ------------------------------------------------------------------ loading
+    def _load_puzzle(self, index):
+        """SPaRC_Gym.py:95-217 (fresh planes; see module docstring)."""
+        puzzle = self.puzzles[index]
+        self.difficulty = puzzle["difficulty"]
+        self.polyshapes = puzzle["polyshapes"]
+        self.x_size, self.y_size = puzzle["x_size"], puzzle["y_size"]
+        self.obs_array = OrderedDict((k, v.copy()) for k, v in puzzle["obs_array"].items())
+        self.color_array = puzzle["color_array"]
+        self.additional_info = puzzle["additional_info"]
+        if self.observation == "SPaRC":                                              # 153-164
+            raw = puzzle["observ"]
+            if isinstance(raw, np.ndarray) and raw.dtype == object and raw.ndim == 1:
+                grid_rows = [r.astype(str).tolist() for r in raw]
+            elif isinstance(raw, np.ndarray) and raw.ndim == 2:
+                grid_rows = raw.astype(str).tolist()
+            else:
+                grid_rows = [[str(c) for c in row] for row in raw]
+            w = len(grid_rows[0])
+            if any(len(r) != w for r in grid_rows):
+                raise ValueError("Non-rectangular SPaRC grid")
+            self.observ = grid_rows
+        self.start_location = puzzle["start_location"]
+        self.target_location = puzzle["target_location"]
+        self.solution_paths = puzzle["solution_paths"]
+        self.solution_count = puzzle["solution_count"]
+        self.path = [[self.start_location[0], self.start_location[1]]]
+        self.normal_reward = 0
+        self.outcome_reward = 0
+        self.rule_status = {}
+        self._agent_location = np.array([self.start_location[0], self.start_location[1]], dtype=np.int32)
+        self._target_location = np.array([self.target_location[0], self.target_location[1]], dtype=np.int32)
+
+        flags = self._core.reset_host(np.array([index], np.uint32))
+        self._legal = int(flags[0] >> 2) & 0xF
+        self._sync_planes()
+        self.obs_array["target_location"][self._target_location[0], self._target_location[1]] = 1
+
+        if self.observation == "new":                                                # 190-196
+            keys = list(self.obs_array.keys())
+            self.observation_space = Dict({
+                "base": Dict({k: Box(low=0, high=1, shape=(self.x_size, self.y_size), dtype=np.int32) for k in keys}),
+                "color": Box(low=0, high=8, shape=(self.x_size, self.y_size), dtype=np.int32),
+                "additional_info": Box(low=0, high=143632, shape=(self.x_size, self.y_size), dtype=np.int64),
+            })
+        elif self.observation == "SPaRC":                                            # 198-204
+            init_json = self._build_json_obs()
+            charset = "".join(sorted(set(init_json) | set("LV.")))
+            self._json_charset = charset
+            self.observation_space = Text(max_length=int(len(init_json) * 2), charset=charset)
+        else:
+            raise ValueError("Invalid observation type. Choose 'new' or 'SPaRC'.")
+        self.action_space = Discrete(4)                                              # 210
+        self._action_to_direction = {0: np.array([1, 0]), 1: np.array([0, -1]),
+                                     2: np.array([-1, 0]), 3: np.array([0, 1])}
+
+    def _sync_planes(self):
+        """Mirror visited / agent_location planes from the device state."""
+        st = self._core.read_state()
+        X, Y, pitch = self.x_size, self.y_size, self._core.table.pitch
+        bits = st["visited"][:, 0]
+        xs, ys = np.meshgrid(np.arange(X), np.arange(Y), indexing="ij")
+        b = (xs * pitch + ys).astype(np.uint64)
+        vis = ((bits[(b >> np.uint64(6)).astype(np.int64)] >> (b & np.uint64(63))) & np.uint64(1)).astype(np.int32)
+        self.obs_array["visited"][...] = vis
+        agent = self.obs_array["agent_location"]
+        agent[...] = 0
+        x, y = int(st["x"][0]), int(st["y"][0])
+        agent[x, y] = 1
+        self.current_step = int(st["step"][0])
+        self.outcome_reward = int(st["outcome"][0])
+        return x, y, int(st["path_len"][0])
+
+    # ------------------------------------------------------------------ gym API
+    def reset(self, seed=None, options=None):
+        """SPaRC_Gym.py:1057-1108."""
+        super().reset(seed=seed)
+        if options is not None:
+            puzzle_id = options.get("puzzle_id", None)
+            for idx, puzzle in enumerate(self.puzzles):
+                if puzzle["id"] == puzzle_id:
+                    self.current_puzzle_index = idx
+                    break
+        elif seed is not None:
+            self.current_puzzle_index = int(self.np_random.integers(len(self.puzzles)))
+        else:
+            self.current_puzzle_index = (self.current_puzzle_index + 1) % len(self.puzzles)
+        self.current_step = 0
+        self._load_puzzle(self.current_puzzle_index)
+        return self._get_obs(), self._get_info()
+
+    def step(self, action):
+        """SPaRC_Gym.py:1111-1238; the transition runs in the HIP step kernel."""
+        codes, flags = self._core.step_host(np.array([action_code(action)], np.uint8))
+        old = (int(self._agent_location[0]), int(self._agent_location[1]))
+        x, y, plen = self._sync_planes()
+        if (x, y) != old:
+            if plen < len(self.path):                                                # traceback pop
+                if self.observation == "SPaRC":
+                    self.observ[old[1]][old[0]] = "." if self.obs_array["gaps"][old[0], old[1]] == 1 else "+"
+                del self.path[-1]
+            else:
+                if self.observation == "SPaRC":
+                    self.observ[old[1]][old[0]] = "V"
+                self.path.append([x, y])
+            if self.observation == "SPaRC":
+                self.observ[y][x] = "L"
+            self._agent_location = np.array([x, y], dtype=np.int64)
+        f = int(flags[0])
+        terminated, truncated = bool(f & 1), bool(f & 2)
+        self._legal = (f >> 2) & 0xF
+        self.normal_reward = reward_value(codes[0])
+        return self._get_obs(), self.normal_reward, terminated, truncated, self._get_info()
+
+    def _get_obs(self):
+        if self.observation == "new":                                                # 978-979
+            return {"base": self.obs_array, "color": self.color_array, "additional_info": self.additional_info}
+        if self.observation == "SPaRC":
+            return self._build_json_obs()
+        raise ValueError("Invalid observation type. Choose 'new' or 'SPaRC'.")
+
+    def _build_json_obs(self):
+        return json.dumps(self.observ, separators=(",", ":"))
+
+    def _get_legal_actions(self):
+        return [a for a in range(4) if (self._legal >> a) & 1]
+
+    def _get_info(self):
+        """SPaRC_Gym.py:994-1022 (rule_status out of scope: {})."""
+        return {"solution_count": self.solution_count,
+                "difficulty": self.difficulty,
+                "grid_x_size": self.x_size,
+                "grid_y_size": self.y_size,
+                "legal_actions": self._get_legal_actions(),
+                "current_step": self.current_step,
+                "agent_location": self._agent_location,
+                "rule_status": self.rule_status,
+                "Rewards": {"normal_reward": self.normal_reward, "outcome_reward": self.outcome_reward}}
+
+    def render(self):
+        return None
+
+    def close(self):
+        """SPaRC_Gym.py:1301-1311 closes only the renderers; the env stays usable."""
+        return None

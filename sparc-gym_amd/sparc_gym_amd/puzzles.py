@@ -1,0 +1,251 @@
+"""Host-side puzzle loading and packing.
+
+``process_puzzles`` restates the reference's one-time preprocessing
+``SPaRC_Gym._process_puzzles`` (SPaRC_Gym/SPaRC_Gym.py:219-368) exactly, including its quirks:
+
+* the loop variable ``symbol`` is never reset per cell or per puzzle, so a property key that
+  is not ``type``/``dot`` (``gap``, ``color``, ...) re-uses the previous cell's (or previous
+  puzzle's) symbol and may add a zero plane of that name (283-306, 334-343);
+* a pool whose first property key is neither ``type`` nor ``dot`` raises UnboundLocalError;
+* every cell centre (odd, odd) is marked in ``gaps`` (345-351).
+
+``pack_table`` turns processed puzzles into the device table of include/sparc_gym_amd.h:
+an ``open`` bitboard (in lattice and not a gap), start/target, and a solution-prefix trie
+over the first ``solution_count`` solutions (the ones ``range(self.solution_count)`` visits at
+SPaRC_Gym.py:1205 and 1217).
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+from dataclasses import dataclass
+
+import numpy as np
+import yaml
+
+COLOR_TO_NUMBER = {"red": 1, "blue": 2, "yellow": 3, "green": 4, "black": 5, "purple": 6,
+                   "orange": 7, "white": 8}   # SPaRC_Gym.py:310
+BASE_KEYS = ("visited", "gaps", "agent_location", "target_location")
+_NONE = 0xFFFF
+_DIRS = ((1, 0), (0, -1), (-1, 0), (0, 1))   # right, up, left, down (SPaRC_Gym.py:212-217)
+_UNBOUND = object()
+
+
+def _rows(df):
+    """Per-row column access for a pandas DataFrame (df[col][i], as the reference) or records."""
+    if hasattr(df, "columns"):
+        n = len(df)
+        cols = list(df.columns)
+        return n, (lambda c, i: df[c][i]), cols
+    recs = list(df)
+    cols = list(recs[0].keys()) if recs else []
+    return len(recs), (lambda c, i: recs[i][c]), cols
+
+
+def process_puzzles(df, observation="new"):
+    """Restatement of SPaRC_Gym._process_puzzles (SPaRC_Gym.py:219-368).
+
+    Returns a list of dicts with the reference's keys: difficulty, x_size, y_size,
+    solution_count, solution_paths, polyshapes, start_location, target_location, obs_array
+    (ordered planes), color_array, additional_info, id (+ observ for observation='SPaRC').
+    """
+    n, get, _ = _rows(df)
+    puzzles = []
+    symbol = _UNBOUND
+
+    def sym():
+        if symbol is _UNBOUND:
+            raise UnboundLocalError("local variable 'symbol' referenced before assignment")
+        return symbol
+
+    for i in range(n):
+        puzzle = {}
+        puzzle["difficulty"] = get("difficulty_level", i)                          # 239-240
+        grid_size = get("grid_size", i)                                             # 243-248
+        x_size = grid_size["width"] * 2 + 1
+        y_size = grid_size["height"] * 2 + 1
+        puzzle["x_size"], puzzle["y_size"] = x_size, y_size
+        solution_count = get("solution_count", i)                                   # 251-257
+        solution_paths = [[[pt["x"], pt["y"]] for pt in item["path"]] for item in get("solutions", i)]
+        puzzle["solution_count"], puzzle["solution_paths"] = solution_count, solution_paths
+        puzzle["polyshapes"] = yaml.safe_load(get("polyshapes", i))                 # 260-262
+        text_yaml = yaml.safe_load(get("text_visualization", i))                    # 265-269
+        puzzle["start_location"] = (text_yaml["puzzle"]["start"]["x"], text_yaml["puzzle"]["start"]["y"])
+        puzzle["target_location"] = (text_yaml["puzzle"]["end"]["x"], text_yaml["puzzle"]["end"]["y"])
+
+        obs_array = OrderedDict((k, np.zeros((x_size, y_size), dtype=np.int32)) for k in BASE_KEYS)
+        color_array = np.zeros((x_size, y_size), dtype=np.int32)                    # 279-280
+        additional_info = np.zeros((x_size, y_size), dtype=np.int64)
+
+        for cell in text_yaml["puzzle"]["cells"]:                                   # 283-325
+            properties = cell.get("properties", {})
+            count = shape = color = None
+            for key, value in properties.items():
+                if key == "type":
+                    symbol = f"{value}"
+                    color = properties.get("color", "")
+                    if value == "triangle":
+                        count = properties.get("count", "")
+                    elif value not in ("star", "square"):
+                        shape = properties.get("polyshape", "")
+                elif key == "dot":
+                    symbol = "dot"
+                if sym() not in obs_array:
+                    obs_array[symbol] = np.zeros((x_size, y_size), dtype=np.int32)
+                if color:
+                    position = cell.get("position", {})
+                    x, y = position.get("x"), position.get("y")
+                    for color_ in COLOR_TO_NUMBER:
+                        if color_ == color:
+                            color_array[x][y] = COLOR_TO_NUMBER[color_]
+                if count:
+                    position = cell.get("position", {})
+                    additional_info[position.get("x")][position.get("y")] = count
+                elif shape:
+                    position = cell.get("position", {})
+                    additional_info[position.get("x")][position.get("y")] = shape
+
+        for cell in text_yaml["puzzle"]["cells"]:                                   # 329-343
+            position = cell.get("position", {})
+            properties = cell.get("properties", {})
+            x, y = position.get("x"), position.get("y")
+            for key, value in properties.items():
+                if key == "type":
+                    symbol = f"{value}"
+                elif key == "dot":
+                    symbol = "dot"
+                elif key == "gap":
+                    symbol = "gaps"
+                if sym() in obs_array:
+                    obs_array[symbol][x, y] = 1
+
+        for k in range(x_size - 1):                                                 # 345-351
+            for j in range(y_size - 1):
+                if k % 2 == 1 and j % 2 == 1:
+                    obs_array["gaps"][k, j] = 1
+
+        puzzle["obs_array"] = obs_array
+        puzzle["color_array"] = color_array
+        puzzle["additional_info"] = additional_info
+        if observation == "SPaRC":                                                  # 358-360
+            puzzle["observ"] = get("puzzle_array", i)
+        puzzle["id"] = get("id", i)                                                 # 362-363
+        puzzles.append(puzzle)
+    return puzzles
+
+
+# ----------------------------------------------------------------------------------- packing
+@dataclass
+class PuzzleTable:
+    """Device puzzle table (layout documented in include/sparc_gym_amd.h)."""
+    open: np.ndarray        # uint64 [P][words]
+    info: np.ndarray        # uint32 [P][4]
+    trie: np.ndarray        # uint32 [nodes][4]
+    pitch: int
+    words: int
+    x_max: int
+    y_max: int
+
+    @property
+    def num_puzzles(self):
+        return len(self.info)
+
+
+def lattice_geometry(puzzles, pitch=None, words=None):
+    x_max = max(int(p["x_size"]) for p in puzzles)
+    y_max = max(int(p["y_size"]) for p in puzzles)
+    pitch = y_max if pitch is None else int(pitch)
+    if pitch < y_max:
+        raise ValueError(f"pitch {pitch} < max y_size {y_max}")
+    bits = (x_max - 1) * pitch + y_max
+    need = 1 if bits <= 64 else 2 if bits <= 128 else 4 if bits <= 256 else None
+    if need is None or x_max > 255:
+        raise ValueError(f"lattice {x_max}x{y_max} exceeds the 256-bit bitboard (15x15 lattices max)")
+    words = need if words is None else int(words)
+    if words not in (1, 2, 4) or words < need:
+        raise ValueError(f"words={words} cannot hold a {x_max}x{pitch} lattice")
+    return pitch, words, x_max, y_max
+
+
+def _int_coord(v):
+    f = float(v)
+    if f != int(f):
+        return None
+    return int(f)
+
+
+def build_trie(start, solutions):
+    """Solution-prefix trie.  Node 0 is the one-point path [start].  Returns
+    (nodes list of [c0, c1, c2, c3, parent, terminal, depth], root_valid)."""
+    nodes = [[_NONE, _NONE, _NONE, _NONE, _NONE, 0, 0]]
+    root_valid = False
+    for sol in solutions:
+        pts = [(_int_coord(a), _int_coord(b)) for a, b in sol]
+        if not pts or pts[0] != tuple(start) or None in pts[0]:
+            continue                          # never equal to / extended by [start, ...]
+        root_valid = True
+        cur, complete = 0, True
+        for (ax, ay), (bx, by) in zip(pts[:-1], pts[1:]):
+            if ax is None or bx is None or ay is None or by is None:
+                complete = False
+                break
+            d = _DIRS.index((bx - ax, by - ay)) if (bx - ax, by - ay) in _DIRS else None
+            if d is None:                     # the agent only moves to a neighbour: this
+                complete = False              # solution's remaining points are unreachable
+                break
+            nxt = nodes[cur][d]
+            if nxt == _NONE:
+                nxt = len(nodes)
+                nodes.append([_NONE, _NONE, _NONE, _NONE, cur, 0, nodes[cur][6] + 1])
+                nodes[cur][d] = nxt
+            cur = nxt
+        if complete:
+            nodes[cur][5] = 1
+    if len(nodes) > _NONE:
+        raise ValueError("solution trie exceeds 65535 nodes for one puzzle")
+    return nodes, root_valid
+
+
+def pack_table(puzzles, pitch=None, words=None):
+    """Processed puzzles -> PuzzleTable (numpy, host)."""
+    pitch, words, x_max, y_max = lattice_geometry(puzzles, pitch, words)
+    P = len(puzzles)
+    open_ = np.zeros((P, words), np.uint64)
+    info = np.zeros((P, 4), np.uint32)
+    tries = []
+    base = 0
+    for q, p in enumerate(puzzles):
+        X, Y = int(p["x_size"]), int(p["y_size"])
+        sx, sy = (int(v) for v in p["start_location"])
+        tx, ty = (int(v) for v in p["target_location"])
+        if not (0 <= sx < X and 0 <= sy < Y and 0 <= tx < X and 0 <= ty < Y):
+            raise ValueError(f"puzzle {q}: start/target outside the {X}x{Y} lattice")
+        gaps = np.asarray(p["obs_array"]["gaps"])
+        xs, ys = np.nonzero(gaps[:X, :Y] == 0)
+        bits = xs.astype(np.int64) * pitch + ys
+        words_arr = np.zeros(words, np.uint64)
+        for w in range(words):
+            sel = bits[(bits >> 6) == w] & 63
+            words_arr[w] = np.bitwise_or.reduce(np.left_shift(np.uint64(1), sel.astype(np.uint64)),
+                                                initial=np.uint64(0))
+        open_[q] = words_arr
+        nsol = int(p["solution_count"])
+        sols = p["solution_paths"]
+        if nsol > len(sols):
+            # the reference raises IndexError lazily at SPaRC_Gym.py:1206/1218; refuse up front
+            raise ValueError(f"puzzle {q}: solution_count {nsol} > {len(sols)} stored solutions")
+        nodes, root_valid = build_trie((sx, sy), sols[:max(nsol, 0)])
+        flags = (1 if nsol > 0 else 0) | (2 if root_valid else 0)
+        info[q, 0] = X | (Y << 8) | (sx << 16) | (sy << 24)
+        info[q, 1] = tx | (ty << 8) | (flags << 16)
+        if root_valid:
+            info[q, 2], info[q, 3] = base, len(nodes)
+            arr = np.asarray(nodes, np.uint32)
+            rec = np.zeros((len(nodes), 4), np.uint32)
+            rec[:, 0] = arr[:, 0] | (arr[:, 1] << 16)
+            rec[:, 1] = arr[:, 2] | (arr[:, 3] << 16)
+            rec[:, 2] = arr[:, 4] | (arr[:, 5] << 16)
+            rec[:, 3] = arr[:, 6]
+            tries.append(rec)
+            base += len(nodes)
+    trie = np.concatenate(tries) if tries else np.zeros((0, 4), np.uint32)
+    return PuzzleTable(open_, info, np.ascontiguousarray(trie), pitch, words, x_max, y_max)

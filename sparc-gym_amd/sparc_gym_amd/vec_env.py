@@ -1,0 +1,192 @@
+"""SPaRCVecEnv: thousands of SPaRC envs stepped together on one MI355X.
+
+The batched form of the reference's ``reset()/step()`` (SPaRC_Gym.py:1057-1238).  State lives in
+HBM as a structure of arrays owned by the C context; every call is one HIP launch on the
+caller's torch stream, and results stay on the GPU as torch tensors (no host round trip).
+
+    vec = SPaRCVecEnv(65536, puzzles=records, traceback=True)
+    obs, info = vec.reset(seed=0)
+    obs, reward, terminated, truncated, info = vec.step(actions)   # actions: [N] on the GPU
+    out = vec.rollout(T, actions=None, seed=1)                      # T steps in one launch
+
+Autoreset follows gymnasium's next-step convention by default: the step after an env
+terminates/truncates resets it onto the next puzzle ((index + 1) % P, the reference's plain
+``reset()`` at SPaRC_Gym.py:1087) and ignores that step's action.  ``autoreset='none'``
+reproduces the reference exactly (stepping past the end keeps the finished state).
+
+Observations (``observation='new'``): ``visited`` and ``agent_location`` as int32 planes
+[N, x_dim, y_dim] (padded lattice) written by the obs-pack kernel, plus ``puzzle_index``; the
+static planes (gaps, target, symbols, color, additional_info) of every puzzle are in
+``static_planes`` and ``static_keys`` (``static_planes[puzzle_index]`` gives an env's).
+``observation='compact'`` returns only ``puzzle_index`` and the agent location.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .core import SparcCore
+from .env import load_puzzle_source
+from .puzzles import pack_table, process_puzzles
+
+# reward code -> float64 value; code/100 in float64 is exactly the reference's 0.01/-0.01 double
+REWARD_SCALE = 100.0
+
+
+class SPaRCVecEnv:
+    def __init__(self, num_envs, puzzles=None, df_name="lkaesberg/SPaRC", df_split="all", df_set="test",
+                 observation="new", traceback=False, max_steps=2000, autoreset="next_step", device=0,
+                 env_offset=0, pitch=None, words=None, processed=None, table=None):
+        if observation not in ("new", "compact"):
+            raise ValueError("observation must be 'new' or 'compact' for the vector env")
+        self.num_envs = int(num_envs)
+        self.observation = observation
+        self.traceback = bool(traceback)
+        self.max_steps = max_steps
+        self.autoreset = autoreset
+        self.device = torch.device("cuda", device)
+        if processed is None:
+            processed = process_puzzles(load_puzzle_source(puzzles, df_name, df_split, df_set))
+        self.puzzles = processed
+        self.table = table if table is not None else pack_table(processed, pitch, words)
+        self.num_puzzles = self.table.num_puzzles
+        self.core = SparcCore(self.table, self.num_envs, traceback, max_steps, autoreset, device, env_offset)
+        self.x_dim, self.y_dim = self.table.x_max, self.table.y_max
+        n, dev = self.num_envs, self.device
+        self._act = torch.empty(n, dtype=torch.uint8, device=dev)
+        self._rew = torch.empty(n, dtype=torch.int8, device=dev)
+        self._flags = torch.empty(n, dtype=torch.uint8, device=dev)
+        self._pidx = torch.empty(n, dtype=torch.int32, device=dev)
+        self._pos = torch.empty(n, dtype=torch.int32, device=dev)
+        if observation == "new":
+            self._vis = torch.empty((n, self.x_dim, self.y_dim), dtype=torch.int32, device=dev)
+            self._agent = torch.empty_like(self._vis)
+            self._build_static()
+        self._cursor = np.arange(n, dtype=np.int64) % self.num_puzzles   # "__init__ loads" env i -> i mod P
+        self._np_random = None
+        self._bound_stream = None
+
+    # ------------------------------------------------------------------ helpers
+    def _stream(self):
+        s = torch.cuda.current_stream(self.device)
+        if self._bound_stream != s.cuda_stream:
+            self.core.set_stream(s.cuda_stream)
+            self._bound_stream = s.cuda_stream
+        return s
+
+    def _build_static(self):
+        keys = []
+        for p in self.puzzles:
+            for k in p["obs_array"]:
+                if k not in keys and k not in ("visited", "agent_location"):
+                    keys.append(k)
+        self.static_keys = keys + ["color", "additional_info"]
+        P, X, Y = self.num_puzzles, self.x_dim, self.y_dim
+        st = np.zeros((P, len(self.static_keys), X, Y), np.int64)
+        for q, p in enumerate(self.puzzles):
+            px, py = p["x_size"], p["y_size"]
+            for j, k in enumerate(keys):
+                if k in p["obs_array"]:
+                    st[q, j, :px, :py] = p["obs_array"][k]
+            tx, ty = p["target_location"]
+            st[q, keys.index("target_location"), :, :] = 0
+            st[q, keys.index("target_location"), tx, ty] = 1
+            st[q, -2, :px, :py] = p["color_array"]
+            st[q, -1, :px, :py] = p["additional_info"]
+        self.static_planes = torch.from_numpy(st).to(self.device)
+
+    def _obs(self):
+        self.core.copy_state_device(4, self._pidx.data_ptr())
+        self.core.copy_state_device(1, self._pos.data_ptr())
+        loc = torch.stack([self._pos & 0xFF, (self._pos >> 8) & 0xFF], dim=1)
+        if self.observation == "compact":
+            return {"puzzle_index": self._pidx, "agent_location": loc}
+        self.core.obs_pack_device(self._vis.data_ptr(), self._agent.data_ptr(), self.x_dim, self.y_dim)
+        return {"visited": self._vis, "agent_location": self._agent, "puzzle_index": self._pidx,
+                "agent_xy": loc}
+
+    @property
+    def np_random(self):
+        if self._np_random is None:
+            self._np_random = np.random.Generator(np.random.PCG64(np.random.SeedSequence()))
+        return self._np_random
+
+    # ------------------------------------------------------------------ API
+    def reset(self, seed=None, options=None):
+        """Per-env puzzle choice as SPaRC_Gym.reset (SPaRC_Gym.py:1075-1087), vectorised:
+        options['puzzle_index'] ([N] ints) or options['puzzle_id'] ([N] ids) > seed
+        (Generator(PCG64(SeedSequence(seed))).integers(P, size=N)) > sequential (+1 mod P)."""
+        self._stream()
+        P = self.num_puzzles
+        if options is not None and "puzzle_index" in options:
+            q = np.asarray(options["puzzle_index"], np.int64)
+        elif options is not None and "puzzle_id" in options:
+            ids = {p["id"]: i for i, p in reversed(list(enumerate(self.puzzles)))}
+            want = options["puzzle_id"]
+            want = [want] * self.num_envs if isinstance(want, str) else list(want)
+            q = np.array([ids.get(w, c) for w, c in zip(want, self._cursor)], np.int64)
+        elif seed is not None:
+            self._np_random = np.random.Generator(np.random.PCG64(np.random.SeedSequence(seed)))
+            q = self._np_random.integers(P, size=self.num_envs)
+        else:
+            q = (self._cursor + 1) % P
+        if q.shape != (self.num_envs,) or q.min() < 0 or q.max() >= P:
+            raise ValueError("puzzle indices must be [num_envs] in [0, num_puzzles)")
+        self._cursor = q.copy()
+        flags = self.core.reset_host(q.astype(np.uint32))
+        info = {"legal_mask": torch.from_numpy(((flags >> 2) & 0xF).astype(np.uint8)).to(self.device)}
+        return self._obs(), info
+
+    def step(self, actions):
+        """One step() of every env: actions [N] (int; >= 4 is illegal = no move)."""
+        s = self._stream()
+        a = torch.as_tensor(actions, device=self.device)
+        if a.shape != (self.num_envs,):
+            raise ValueError(f"actions must have shape ({self.num_envs},)")
+        if a.dtype != torch.uint8:
+            a = torch.where((a >= 0) & (a < 4), a, torch.full_like(a, 255)).to(torch.uint8)
+        with torch.cuda.stream(s):
+            self._act.copy_(a)
+        self.core.step_device(self._act.data_ptr(), self._rew.data_ptr(), self._flags.data_ptr())
+        f = self._flags
+        reward = self._rew.to(torch.float64) / REWARD_SCALE
+        terminated = (f & 1).bool()
+        truncated = (f & 2).bool()
+        info = {"legal_mask": (f >> 2) & 0xF, "autoreset": (f & 64).bool(), "reward_code": self._rew}
+        return self._obs(), reward, terminated, truncated, info
+
+    def rollout(self, T, actions=None, seed=0, t0=0, stats=None, record=True, out=None):
+        """T steps of every env in ONE kernel launch.  actions: [T, N] uint8 on the GPU or None
+        (counter-based random actions, sparc_rand_action(seed, env_offset + i, t0 + t)).
+        Returns reward codes and flags [T, N] (int8 / uint8) if ``record`` (written into
+        ``out=(reward_code, flags)`` when given)."""
+        self._stream()
+        n = self.num_envs
+        if actions is not None:
+            actions = torch.as_tensor(actions, device=self.device)
+            if actions.shape != (T, n) or actions.dtype != torch.uint8 or not actions.is_contiguous():
+                raise ValueError(f"actions must be a contiguous uint8 tensor of shape ({T}, {n})")
+        rew = flags = None
+        if out is not None:
+            rew, flags = out
+            for t_, dt in ((rew, torch.int8), (flags, torch.uint8)):
+                if t_.shape != (T, n) or t_.dtype != dt or not t_.is_contiguous() or t_.device != self.device:
+                    raise ValueError(f"out tensors must be contiguous [{T}, {n}] int8 / uint8 on {self.device}")
+        elif record:
+            rew = torch.empty((T, n), dtype=torch.int8, device=self.device)
+            flags = torch.empty((T, n), dtype=torch.uint8, device=self.device)
+        if stats is not None and (stats.shape != (n, 4) or stats.dtype != torch.int32 or not stats.is_contiguous()):
+            raise ValueError("stats must be a contiguous int32 tensor [N, 4]")
+        self.core.rollout_device(T, None if actions is None else actions.data_ptr(),
+                                 None if rew is None else rew.data_ptr(),
+                                 None if flags is None else flags.data_ptr(),
+                                 None if stats is None else stats.data_ptr(), seed, t0)
+        return {"reward_code": rew, "flags": flags}
+
+    def state(self):
+        """Host snapshot of the per-env state (x, y, path_len, step, puzzle, outcome, visited bits)."""
+        torch.cuda.current_stream(self.device).synchronize()
+        return self.core.read_state()
+
+    def close(self):
+        self.core.close()

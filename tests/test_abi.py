@@ -1,0 +1,56 @@
+"""The C-ABI library loads on the CPU host and exports every symbol include/ declares."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from sparc_gym_amd import _lib
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "sparc_gym_amd.h")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^\s*(?:int|const char \*|void)\s*\*?\s*(sparc_\w+)\s*\(", src, flags=re.M)
+    return sorted(set(names))
+
+
+def test_header_declares_the_bound_symbols():
+    assert set(declared_symbols()) == set(_lib.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    for name in declared_symbols():
+        assert hasattr(lib, name), name
+    assert lib.sparc_abi_version() == 1
+
+
+def test_create_validates_before_touching_a_device():
+    lib = _lib.load()
+    ctx = ctypes.c_void_p()
+    bad = _lib.SparcConfig(0, 0, 100, 0, 7, 1, 0)
+    assert lib.sparc_create(0, ctypes.byref(bad), ctypes.byref(ctx)) == -1
+    assert b"num_envs" in lib.sparc_last_error(None)
+    bad = _lib.SparcConfig(4, 0, 100, 0, 7, 3, 0)
+    assert lib.sparc_create(0, ctypes.byref(bad), ctypes.byref(ctx)) == -1
+    assert ctx.value is None
+
+
+def test_null_context_is_an_error_not_a_crash():
+    lib = _lib.load()
+    assert lib.sparc_step_device(None, None, None, None) != 0
+    assert lib.sparc_sync(None) != 0
+    assert lib.sparc_destroy(None) == 0
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    with pytest.raises(ImportError):
+        _lib._lib = None
+        try:
+            _lib.load(str(tmp_path / "nope.so"))
+        finally:
+            _lib._lib = None

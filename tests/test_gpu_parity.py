@@ -1,0 +1,264 @@
+"""GPU parity: the HIP step path (through the C ABI) against the reference's golden vectors and
+against the C oracle at batch sizes up to the benchmark's 65,536 envs.  Bit-exact throughout:
+reward codes, flags, positions, step counters and visited bitboards are integers."""
+import zlib
+
+import numpy as np
+import pytest
+
+import golden_io
+from oracle import COracle
+from sparc_gym_amd import synthetic
+from sparc_gym_amd.puzzles import pack_table, process_puzzles
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def _code(v):
+    return int(round(float(v) * 100))
+
+
+def oracle_pool_from_processed(proc):
+    return [{"x_size": p["x_size"], "y_size": p["y_size"], "start": list(p["start_location"]),
+             "target": list(p["target_location"]), "solution_count": p["solution_count"],
+             "solution_paths": p["solution_paths"], "gaps": p["obs_array"]["gaps"]} for p in proc]
+
+
+# ----------------------------------------------------------------------------- golden vectors
+@pytest.mark.parametrize("pool", golden_io.POOLS)
+def test_single_env_matches_reference(on_gpu, pool):
+    """SPaRC_Gym (batch of one on the GPU) reproduces the reference's reset/step outputs."""
+    from sparc_gym_amd import SPaRC_Gym
+    g = golden_io.load(pool)
+    env = SPaRC_Gym(puzzles=g["records"], traceback=g["traceback"], max_steps=g["max_steps"])
+    for ep in g["episodes"]:
+        obs, info = env.reset(options={"puzzle_id": ep["puzzle_id"]})
+        assert env.current_puzzle_index == ep["puzzle_index"]
+        ref = ep["reset"]
+        assert list(obs["base"].keys()) == ref["obs"]["base_keys"]
+        for k, plane in ref["obs"]["base"].items():
+            assert np.array_equal(obs["base"][k], golden_io.dense(plane)), k
+        assert np.array_equal(obs["color"], golden_io.dense(ref["obs"]["color"]))
+        assert np.array_equal(obs["additional_info"], golden_io.dense(ref["obs"]["additional_info"]))
+        assert info["legal_actions"] == ref["info"]["legal_actions"]
+        for a, st in zip(ep["actions"], ep["steps"]):
+            obs, r, term, trunc, info = env.step(a)
+            assert repr(r) == st["reward"]["repr"] and type(r).__name__ == st["reward"]["type"]
+            assert (term, trunc) == (st["terminated"], st["truncated"])
+            for k in ("legal_actions", "current_step", "solution_count", "difficulty",
+                      "grid_x_size", "grid_y_size"):
+                assert info[k] == st["info"][k], k
+            assert [int(v) for v in info["agent_location"]] == st["info"]["agent_location"]
+            assert repr(info["Rewards"]["normal_reward"]) == st["info"]["normal_reward"]["repr"]
+            assert repr(info["Rewards"]["outcome_reward"]) == st["info"]["outcome_reward"]["repr"]
+            assert np.array_equal(obs["base"]["visited"], golden_io.dense(st["visited"]))
+            assert np.array_equal(obs["base"]["agent_location"], golden_io.dense(st["agent_plane"]))
+
+
+@pytest.mark.parametrize("pool", golden_io.POOLS)
+def test_vec_env_matches_reference(on_gpu, pool):
+    """All episodes of a pool as one batch through the step kernel (autoreset='none')."""
+    from sparc_gym_amd import SPaRCVecEnv
+    g = golden_io.load(pool)
+    eps = g["episodes"]
+    n, T = len(eps), max(len(e["actions"]) for e in eps)
+    vec = SPaRCVecEnv(n, puzzles=g["records"], traceback=g["traceback"], max_steps=g["max_steps"],
+                      autoreset="none")
+    obs, info = vec.reset(options={"puzzle_index": [e["puzzle_index"] for e in eps]})
+    legal0 = info["legal_mask"].cpu().numpy()
+    for i, e in enumerate(eps):
+        assert [a for a in range(4) if legal0[i] >> a & 1] == e["reset"]["info"]["legal_actions"]
+    acts = np.zeros((T, n), np.int64)
+    for i, e in enumerate(eps):
+        acts[:len(e["actions"]), i] = e["actions"]
+    for t in range(T):
+        obs, rew, term, trunc, info = vec.step(torch.from_numpy(acts[t]).cuda())
+        rew, term, trunc = rew.cpu().numpy(), term.cpu().numpy(), trunc.cpu().numpy()
+        legal = info["legal_mask"].cpu().numpy()
+        vis, agent = obs["visited"].cpu().numpy(), obs["agent_location"].cpu().numpy()
+        for i, e in enumerate(eps):
+            if t >= len(e["steps"]):
+                continue
+            st = e["steps"][t]
+            assert rew[i] == st["reward"]["value"], (pool, i, t)   # float64, bit-exact
+            assert (bool(term[i]), bool(trunc[i])) == (st["terminated"], st["truncated"])
+            assert [a for a in range(4) if legal[i] >> a & 1] == st["info"]["legal_actions"]
+            X, Y = st["visited"]["shape"]
+            assert np.array_equal(vis[i, :X, :Y], golden_io.dense(st["visited"]))
+            assert np.array_equal(agent[i, :X, :Y], golden_io.dense(st["agent_plane"]))
+            assert vis[i, X:].sum() == 0 and vis[i, :, Y:].sum() == 0
+
+
+# ----------------------------------------------------------------------------- vs C oracle
+POOLS = {
+    "7x7_full": dict(sizes=((3, 3),), full_properties=True),
+    "7x7_base": dict(sizes=((3, 3),), full_properties=False),
+    "mixed_5_11": dict(sizes=((2, 2), (3, 3), (4, 4), (5, 5), (2, 5), (5, 3)), full_properties=True),
+    "15x15": dict(sizes=((7, 7), (6, 7)), full_properties=True),
+}
+
+
+def _make(name, n_puzzles=64, seed=0):
+    recs = synthetic.make_puzzles(n_puzzles, seed=seed, **POOLS[name])
+    proc = process_puzzles(recs)
+    return proc, pack_table(proc)
+
+
+def _run_three_ways(proc, table, n, T, tb, max_steps, autoreset, seed):
+    """rollout kernel (one launch) vs T step kernels vs the C oracle, same inputs."""
+    from sparc_gym_amd import SPaRCVecEnv
+    rng = np.random.default_rng(seed)
+    pids = rng.integers(len(proc), size=n)
+    acts = rng.choice(np.array([0, 1, 2, 3, 0, 1, 2, 3, 4, 255], np.uint8), size=(T, n))
+    kw = dict(processed=proc, table=table, traceback=tb, max_steps=max_steps, autoreset=autoreset,
+              observation="compact")
+    a = SPaRCVecEnv(n, **kw)
+    a.reset(options={"puzzle_index": pids})
+    stats = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
+    out = a.rollout(T, torch.from_numpy(acts).cuda(), stats=stats)
+    ra, fa = out["reward_code"].cpu().numpy(), out["flags"].cpu().numpy()
+    sa = a.state()
+
+    b = SPaRCVecEnv(n, **kw)
+    b.reset(options={"puzzle_index": pids})
+    rb, fb = np.zeros((T, n), np.int8), np.zeros((T, n), np.uint8)
+    for t in range(T):
+        _, _, _, _, info = b.step(torch.from_numpy(acts[t]).cuda())
+        rb[t] = info["reward_code"].cpu().numpy()
+        fb[t] = b._flags.cpu().numpy()
+    sb = b.state()
+
+    o = COracle(oracle_pool_from_processed(proc), n, tb, max_steps, autoreset={"none": 0, "next_step": 1}[autoreset])
+    o.reset(pids)
+    ostats = np.zeros((n, 4), np.int32)
+    ro, fo = o.rollout(T, acts, stats=ostats)
+    so = o.state()
+    return (ra, fa, sa, stats.cpu().numpy()), (rb, fb, sb), (ro, fo, so, ostats), table
+
+
+def _assert_states_equal(s_gpu, s_or, table):
+    assert np.array_equal(s_gpu["x"], s_or["x"]) and np.array_equal(s_gpu["y"], s_or["y"])
+    assert np.array_equal(s_gpu["step"], s_or["step"])
+    assert np.array_equal(s_gpu["path_len"], s_or["path_len"])
+    assert np.array_equal(s_gpu["puzzle"], s_or["pid"])
+    assert np.array_equal(s_gpu["outcome"], s_or["outcome"])
+    from sparc_gym_amd.core import visited_planes
+    planes = visited_planes(s_gpu["visited"], table, 16, 16)
+    assert np.array_equal(planes, s_or["visited"].astype(np.int32))
+
+
+@pytest.mark.parametrize("name", list(POOLS))
+@pytest.mark.parametrize("tb", [False, True])
+@pytest.mark.parametrize("autoreset", ["next_step", "none"])
+def test_rollout_step_oracle_agree(on_gpu, name, tb, autoreset):
+    proc, table = _make(name, seed=len(name))
+    max_steps = 2000 if autoreset == "next_step" else 150
+    (ra, fa, sa, st_a), (rb, fb, sb), (ro, fo, so, st_o), table = _run_three_ways(
+        proc, table, 2048, 257, tb, max_steps, autoreset, seed=zlib.crc32(f"{name}{tb}".encode()))
+    assert np.array_equal(ra, ro) and np.array_equal(fa, fo)
+    assert np.array_equal(rb, ro) and np.array_equal(fb, fo)
+    assert np.array_equal(st_a, st_o)
+    _assert_states_equal(sa, so, table)
+    _assert_states_equal(sb, so, table)
+
+
+def test_random_action_rollout_matches_oracle(on_gpu):
+    """Device counter-based actions == oracle's restatement of the same hash."""
+    from sparc_gym_amd import SPaRCVecEnv
+    proc, table = _make("7x7_full", seed=5)
+    n, T = 4096, 300
+    pids = np.arange(n) % len(proc)
+    v = SPaRCVecEnv(n, processed=proc, table=table, traceback=True, observation="compact", env_offset=12345)
+    v.reset(options={"puzzle_index": pids})
+    out = v.rollout(T, None, seed=99, t0=7)
+    o = COracle(oracle_pool_from_processed(proc), n, True, 2000, autoreset=1)
+    o.reset(pids)
+    ro, fo = o.rollout(T, None, seed=99, env_offset=12345, t0=7)
+    assert np.array_equal(out["reward_code"].cpu().numpy(), ro)
+    assert np.array_equal(out["flags"].cpu().numpy(), fo)
+
+
+def test_chunked_rollouts_equal_one_launch(on_gpu):
+    """State round-trips HBM between launches bit-exactly (T=100 + 57 + 1 == T=158)."""
+    from sparc_gym_amd import SPaRCVecEnv
+    proc, table = _make("mixed_5_11", seed=2)
+    n = 3000
+    pids = np.arange(n) % len(proc)
+    acts = torch.randint(0, 4, (158, n), dtype=torch.uint8, device="cuda")
+    kw = dict(processed=proc, table=table, traceback=True, observation="compact")
+    a = SPaRCVecEnv(n, **kw)
+    a.reset(options={"puzzle_index": pids})
+    full = a.rollout(158, acts)
+    b = SPaRCVecEnv(n, **kw)
+    b.reset(options={"puzzle_index": pids})
+    parts = [b.rollout(100, acts[:100].contiguous()), b.rollout(57, acts[100:157].contiguous()),
+             b.rollout(1, acts[157:].contiguous())]
+    for key in ("reward_code", "flags"):
+        assert torch.equal(full[key], torch.cat([p[key] for p in parts]))
+
+
+# ----------------------------------------------------------------------------- full size
+def test_full_size_65536_bit_exact_and_invariants(on_gpu):
+    """BASELINE config C3 shape: 65,536 envs, 7x7 full property set, traceback=True."""
+    from sparc_gym_amd import SPaRCVecEnv
+    proc, table = _make("7x7_full", n_puzzles=1024, seed=0)
+    n, T = 65536, 400
+    pids = (np.arange(n, dtype=np.uint64) * 2654435761 % 1024).astype(np.int64)
+    v = SPaRCVecEnv(n, processed=proc, table=table, traceback=True, observation="compact")
+    v.reset(options={"puzzle_index": pids})
+    stats = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
+    out = v.rollout(T, None, seed=2024, stats=stats)
+    r, f = out["reward_code"].cpu().numpy(), out["flags"].cpu().numpy()
+    s = v.state()
+    # size-independent properties
+    assert set(np.unique(r)) <= {-100, -1, 0, 1, 100}
+    assert not np.any((f & 3) == 3)                     # terminated and truncated exclusive
+    st = stats.cpu().numpy()
+    assert np.array_equal(st[:, 0], r.astype(np.int64).sum(0))
+    assert np.array_equal(st[:, 1], ((f & 3) != 0).sum(0))
+    done_prev = np.vstack([np.zeros((1, n), bool), (f[:-1] & 3) != 0])
+    assert np.array_equal((f & 64) != 0, done_prev)     # next-step autoreset exactly after done
+    assert np.all(r[(f & 64) != 0] == 0)
+    pop = np.zeros(n, np.int64)
+    for w in range(table.words):
+        pop += np.array([bin(int(b)).count("1") for b in s["visited"][w]])
+    assert np.array_equal(pop, s["path_len"].astype(np.int64))   # visited == path nodes
+    # and bit-exact against the C oracle at full size
+    o = COracle(oracle_pool_from_processed(proc), n, True, 2000, autoreset=1)
+    o.reset(pids)
+    ro, fo = o.rollout(T, None, seed=2024)
+    assert np.array_equal(r, ro) and np.array_equal(f, fo)
+
+
+def test_obs_pack_matches_state(on_gpu):
+    from sparc_gym_amd import SPaRCVecEnv
+    from sparc_gym_amd.core import visited_planes
+    proc, table = _make("mixed_5_11", seed=8)
+    n = 1000
+    v = SPaRCVecEnv(n, processed=proc, table=table, traceback=True)
+    v.reset(seed=3)
+    v.rollout(37, None, seed=1)
+    obs, *_ = v.step(torch.randint(0, 4, (n,), device="cuda"))
+    s = v.state()
+    vis = obs["visited"].cpu().numpy()
+    assert np.array_equal(vis, visited_planes(s["visited"], table))
+    ag = obs["agent_location"].cpu().numpy()
+    assert np.array_equal(ag.reshape(n, -1).sum(1), np.ones(n))
+    assert np.all(ag[np.arange(n), s["x"], s["y"]] == 1)
+    pidx = obs["puzzle_index"].cpu().numpy()
+    assert np.array_equal(pidx, s["puzzle"].astype(np.int32))
+
+
+def test_device_reset_rejects_bad_index(on_gpu):
+    from sparc_gym_amd import SPaRCVecEnv
+    proc, table = _make("7x7_base", seed=1)
+    v = SPaRCVecEnv(64, processed=proc, table=table, observation="compact")
+    with pytest.raises(ValueError):
+        v.reset(options={"puzzle_index": np.full(64, len(proc))})
+    q = torch.full((64,), len(proc) + 5, dtype=torch.int32, device="cuda")
+    v.reset(options={"puzzle_index": np.zeros(64, np.int64)})
+    v.core.reset_device(q.data_ptr())
+    with pytest.raises(ValueError):
+        v.core.sync()
