@@ -114,8 +114,10 @@ const char *sparc_last_error(const void *ctx);
 /* SPaRC_Gym.__init__ (SPaRC_Gym.py:46-90): allocate the SoA state for num_envs on `device`. */
 int sparc_create(int device, const sparc_config *cfg, void **ctx_out);
 int sparc_destroy(void *ctx);
-/* run on this HIP stream (hipStream_t as void*); NULL = the context's own stream */
+/* run on this HIP stream (hipStream_t as void*; NULL = the HIP null stream).  A new context
+ * runs on its own non-blocking stream; sparc_use_own_stream() returns to it. */
 int sparc_set_stream(void *ctx, void *stream);
+int sparc_use_own_stream(void *ctx);
 int sparc_sync(void *ctx);
 
 /* _process_puzzles output -> device (SPaRC_Gym.py:88, 219-368); host arrays, copied. */

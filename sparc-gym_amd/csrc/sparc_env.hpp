@@ -99,8 +99,8 @@ struct Env {
     uint64_t dirs[D];
     uint64_t open[W];
     uint32_t x, y, len, off, node, outcome, pending, step, pid;
-    uint32_t X, Y, tx, ty, pflags, trie_base;
-    uint4 rec;
+    uint32_t X, Y, tx, ty, pflags, trie_base, trie_cnt;
+    uint4 rec;   // invariant: the trie record of `node` whenever the puzzle's root is valid
 
     __device__ __forceinline__ void load_puzzle(const Params& p, uint32_t q, uint32_t& sx, uint32_t& sy) {
         const uint4 inf = p.tab.info[q];
@@ -112,11 +112,20 @@ struct Env {
         ty = (inf.y >> 8) & 0xFFu;
         pflags = inf.y >> 16;
         trie_base = inf.z;
+        trie_cnt = inf.w;
 #pragma unroll
         for (int k = 0; k < W; ++k) open[k] = p.tab.open[(size_t)q * W + k];
     }
 
-    __device__ __forceinline__ void load_rec(const Params& p) { rec = p.tab.trie[trie_base + node]; }
+    // node < trie_cnt always holds (host-validated tables); the guard turns a broken invariant
+    // into a reported error (sparc_sync) instead of an out-of-bounds read
+    __device__ __forceinline__ void load_rec(const Params& p) {
+        if (node >= trie_cnt) {
+            atomicOr(p.err, 2);
+            node = 0;
+        }
+        rec = p.tab.trie[trie_base + node];
+    }
 
     // _load_puzzle (SPaRC_Gym.py:166-187) with fresh planes
     __device__ __forceinline__ void reset(const Params& p, uint32_t q) {
@@ -272,9 +281,10 @@ struct Env {
         pid = s.pid[i];
         uint32_t sx, sy;
         load_puzzle(p, pid, sx, sy);
-        // the record is needed if this step stays on / returns to the trie; puzzles whose
-        // root is not a prefix (flags bit1 clear) have off >= 1 forever and may have no nodes
-        if (off <= 1 && (pflags & 2u)) load_rec(p);
+        // keep the invariant: pops can bring `off` back to 0 at any later step of a launch.
+        // Puzzles whose root is not a prefix (flags bit1 clear) have off >= 1 forever and may
+        // have no trie nodes at all.
+        if (pflags & 2u) load_rec(p);
         else rec = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, kNone, 0u);
     }
 

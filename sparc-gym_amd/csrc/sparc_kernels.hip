@@ -286,7 +286,14 @@ int sparc_destroy(void* ctx) {
 int sparc_set_stream(void* ctx, void* stream) {
     Ctx* c = static_cast<Ctx*>(ctx);
     if (!c) return fail(nullptr, SPARC_E_INVALID, "null context");
-    c->stream = stream ? static_cast<hipStream_t>(stream) : c->own;
+    c->stream = static_cast<hipStream_t>(stream);   // NULL is the HIP null stream, used as such
+    return SPARC_OK;
+}
+
+int sparc_use_own_stream(void* ctx) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c) return fail(nullptr, SPARC_E_INVALID, "null context");
+    c->stream = c->own;
     return SPARC_OK;
 }
 
@@ -299,6 +306,7 @@ int sparc_sync(void* ctx) {
     HIPCHK(c, hipMemcpy(&e, c->err, sizeof(e), hipMemcpyDeviceToHost));
     if (e) {
         HIPCHK(c, hipMemset(c->err, 0, sizeof(int32_t)));
+        if (e & 2) return fail(c, SPARC_E_STATE, "device-side trie node out of range (state corrupted)");
         return fail(c, SPARC_E_INVALID, "device-side puzzle index out of range in a reset");
     }
     return SPARC_OK;

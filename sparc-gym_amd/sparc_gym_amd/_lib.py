@@ -39,6 +39,7 @@ _SIGS = {
     "sparc_create": ([ctypes.c_int, ctypes.POINTER(SparcConfig), ctypes.POINTER(c_void_p)], c_int32),
     "sparc_destroy": ([c_void_p], c_int32),
     "sparc_set_stream": ([c_void_p, c_void_p], c_int32),
+    "sparc_use_own_stream": ([c_void_p], c_int32),
     "sparc_sync": ([c_void_p], c_int32),
     "sparc_load_puzzles": ([c_void_p, ctypes.POINTER(SparcPuzzleTable)], c_int32),
     "sparc_reset_host": ([c_void_p, c_void_p, c_void_p, c_void_p], c_int32),

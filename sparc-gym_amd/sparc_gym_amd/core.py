@@ -62,7 +62,12 @@ class SparcCore:
         _lib.check(rc, self.ctx)
 
     def set_stream(self, stream_handle):
+        """Order all calls on this HIP stream (int handle; 0 = the null stream, e.g. torch's
+        default stream)."""
         self._check(self.lib.sparc_set_stream(self.ctx, stream_handle or None))
+
+    def use_own_stream(self):
+        self._check(self.lib.sparc_use_own_stream(self.ctx))
 
     def sync(self):
         self._check(self.lib.sparc_sync(self.ctx))
