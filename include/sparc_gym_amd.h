@@ -17,8 +17,10 @@
  *  - One context per GPU, not reentrant; all work is ordered on its stream.
  *
  * Lattice encoding: planes are indexed [x, y] with x_size = 2*width+1, y_size = 2*height+1
- * (SPaRC_Gym.py:243-248).  A point is bit b = x*pitch + y of a `words`-word bitboard, where
- * pitch >= every puzzle's y_size and words*64 >= max x_size * pitch (words in {1, 2, 4}).
+ * (SPaRC_Gym.py:243-248).  A point is bit b = x*pitch + y of a `words`-word bitboard.
+ *  words == 1: padded layout, every puzzle has y_size < pitch <= 15 and
+ *              (x_size + 1) * pitch <= 64 (7x7 / 5x5 pools; the kernels' fast path);
+ *  words 2, 4: pitch >= every y_size and (x_size - 1) * pitch + y_size <= 64 * words.
  *
  * Per-step outputs
  *  reward code  int8  = normal_reward * 100: {-100, -1, 0, +1, +100}  (SPaRC_Gym.py:1201-1223);
@@ -74,11 +76,13 @@ typedef struct {
  *  open  [P][words]  bit set = lattice point inside the puzzle and gaps[x][y] == 0
  *  info  [P][4]      w0 = x_size | y_size<<8 | start_x<<16 | start_y<<24
  *                    w1 = target_x | target_y<<8 | flags<<16
- *                         (flags bit0: solution_count > 0, bit1: some solution starts at start)
+ *                         (flags bit0: solution_count > 0, bit1: some solution starts at start,
+ *                          bit2: the start point is a gap)
  *                    w2 = global index of the puzzle's trie root, w3 = its trie node count
  *  trie  [nodes][4]  solution-prefix trie, local (per puzzle) u16 indices, 0xFFFF = none:
  *                    w0 = child[right] | child[up]<<16, w1 = child[left] | child[down]<<16,
- *                    w2 = parent | terminal<<16, w3 = depth                                  */
+ *                    w2 = parent | terminal<<16 | child_terminal[4]<<17 | parent_terminal<<21,
+ *                    w3 = depth.  Node 0 of each puzzle is the one-point path [start].      */
 typedef struct {
     int32_t num_puzzles;
     int32_t num_nodes;

@@ -6,19 +6,23 @@
 //   x, y        agent location                             self._agent_location
 //   len         len(self.path)
 //   node, off   solution-trie node + off-trie depth        prefix/equality vs solution_paths
-//   rec         trie record of `node` (children, parent, terminal)
+//   node_term   node is a complete solution (valid when off == 0)
+//   rec         trie record of `node`; only read at the NEXT on-trie transition, so the load
+//               issued at a transition overlaps the rest of that step
+//   legal       legal-action mask of the current state (carried from the previous step)
+//   last        direction of the last move (traceback: the only legal revisit is its reverse)
 //   step, outcome, pending, pid
-// plus the puzzle's static row (open bitboard, sizes, start/target, trie base).
+// plus the puzzle's static row (open bitboard, sizes, start/target, trie base) read from a
+// PuzzleSrc: the global table (k_step) or an LDS copy of it (k_rollout).
 //
 // Reference semantics restated (SPaRC_Gym.py):
-//   legal mask  = _get_legal_actions 1024-1051: in bounds, gaps==0, and unvisited or (traceback,
-//                 len>=2, n == path[-2]); path[-2] == pos - dir(last move), so the only legal
-//                 revisit is the reverse of the last move.
+//   legal_mask  = _get_legal_actions 1024-1051: in bounds, gaps==0, and unvisited or (traceback,
+//                 len>=2, n == path[-2]); path[-2] == pos - dir(last move).
 //   advance()   = step 1131-1223: move or traceback-pop, terminated, truncated (max_steps or no
 //                 legal move, cleared when terminated), reward code (x100).
 //   prefix test = _is_on_solution_path 1244-1265 and np.array_equal 1206 via the trie: the path
 //                 is a prefix of some solution iff off == 0; it equals one iff additionally the
-//                 trie node is terminal.  O(1) per step instead of O(S*L).
+//                 node is terminal.  O(1) per step instead of O(S*L).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -26,10 +30,22 @@
 namespace sparc {
 
 constexpr uint32_t kNone = 0xFFFFu;
+constexpr uint32_t kErrPuzzle = 1, kErrTrie = 2;
+
+// trie record w2 fields
+__device__ __forceinline__ uint32_t rec_parent(const uint4& r) { return r.z & 0xFFFFu; }
+__device__ __forceinline__ uint32_t rec_term(const uint4& r) { return (r.z >> 16) & 1u; }
+__device__ __forceinline__ uint32_t rec_child_term(const uint4& r, uint32_t d) { return (r.z >> (17 + d)) & 1u; }
+__device__ __forceinline__ uint32_t rec_parent_term(const uint4& r) { return (r.z >> 21) & 1u; }
+__device__ __forceinline__ uint32_t rec_child(const uint4& r, uint32_t d) {
+    const uint32_t w = d < 2 ? r.x : r.y;
+    return (d & 1) ? (w >> 16) : (w & 0xFFFFu);
+}
 
 struct Table {
     const uint64_t* __restrict__ open;  // [P][W]
     const uint4* __restrict__ info;     // [P]
+    const uint4* __restrict__ root;     // [P] trie record of each puzzle's root (sentinel if none)
     const uint4* __restrict__ trie;     // [nodes]
     uint32_t num_puzzles;
 };
@@ -38,7 +54,7 @@ struct State {                 // SoA, N = num_envs
     uint64_t* __restrict__ vis;   // [W][N]
     uint64_t* __restrict__ dirs;  // [2W][N] (traceback only)
     uint32_t* __restrict__ pos;   // x | y<<8 | len<<16 | off<<24
-    uint32_t* __restrict__ aux;   // node | outcome<<16 (0: 0, 1: +1, 2: -1) | pending<<18
+    uint32_t* __restrict__ aux;   // node | outcome<<16 (0: 0, 1: +1, 2: -1) | pending<<18 | node_term<<19
     uint32_t* __restrict__ step;
     uint32_t* __restrict__ pid;
 };
@@ -52,6 +68,17 @@ struct Params {
     int32_t autoreset;
     uint64_t env_offset;
     int32_t* __restrict__ err;
+};
+
+// Static puzzle rows, from global memory or from an LDS copy (same layout).
+template <int W>
+struct PuzzleSrc {
+    const uint4* info;
+    const uint4* root;
+    const uint64_t* open;
+    __device__ __forceinline__ uint4 get_info(uint32_t q) const { return info[q]; }
+    __device__ __forceinline__ uint4 get_root(uint32_t q) const { return root[q]; }
+    __device__ __forceinline__ uint64_t get_open(uint32_t q, int k) const { return open[(size_t)q * W + k]; }
 };
 
 __device__ __forceinline__ int dir_dx(uint32_t d) { return d == 0 ? 1 : (d == 2 ? -1 : 0); }
@@ -98,12 +125,13 @@ struct Env {
     uint64_t vis[W];
     uint64_t dirs[D];
     uint64_t open[W];
-    uint32_t x, y, len, off, node, outcome, pending, step, pid;
+    uint32_t x, y, len, off, node, node_term, outcome, pending, step, pid, legal, last;
     uint32_t X, Y, tx, ty, pflags, trie_base, trie_cnt;
-    uint4 rec;   // invariant: the trie record of `node` whenever the puzzle's root is valid
+    uint4 rec;
 
-    __device__ __forceinline__ void load_puzzle(const Params& p, uint32_t q, uint32_t& sx, uint32_t& sy) {
-        const uint4 inf = p.tab.info[q];
+    template <class Src>
+    __device__ __forceinline__ void load_puzzle(const Src& src, uint32_t q, uint32_t& sx, uint32_t& sy) {
+        const uint4 inf = src.get_info(q);
         X = inf.x & 0xFFu;
         Y = (inf.x >> 8) & 0xFFu;
         sx = (inf.x >> 16) & 0xFFu;
@@ -114,39 +142,17 @@ struct Env {
         trie_base = inf.z;
         trie_cnt = inf.w;
 #pragma unroll
-        for (int k = 0; k < W; ++k) open[k] = p.tab.open[(size_t)q * W + k];
+        for (int k = 0; k < W; ++k) open[k] = src.get_open(q, k);
     }
 
     // node < trie_cnt always holds (host-validated tables); the guard turns a broken invariant
     // into a reported error (sparc_sync) instead of an out-of-bounds read
     __device__ __forceinline__ void load_rec(const Params& p) {
         if (node >= trie_cnt) {
-            atomicOr(p.err, 2);
+            atomicOr(p.err, (int)kErrTrie);
             node = 0;
         }
         rec = p.tab.trie[trie_base + node];
-    }
-
-    // _load_puzzle (SPaRC_Gym.py:166-187) with fresh planes
-    __device__ __forceinline__ void reset(const Params& p, uint32_t q) {
-        uint32_t sx, sy;
-        pid = q;
-        load_puzzle(p, q, sx, sy);
-        x = sx;
-        y = sy;
-        len = 1;
-        node = 0;
-        off = (pflags & 2u) ? 0u : 1u;  // [start] is a prefix iff some solution begins at start
-        outcome = 0;
-        pending = 0;
-        step = 0;
-#pragma unroll
-        for (int k = 0; k < W; ++k) vis[k] = 0;
-#pragma unroll
-        for (int k = 0; k < D; ++k) dirs[k] = 0;
-        bb_set<W>(vis, x * p.pitch + y);
-        if (off == 0) load_rec(p);
-        else rec = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, kNone, 0u);
     }
 
     __device__ __forceinline__ uint32_t dir_at(uint32_t k) const {
@@ -173,31 +179,54 @@ struct Env {
 
     // _get_legal_actions (SPaRC_Gym.py:1024-1051) as a 4-bit mask in action order
     __device__ __forceinline__ uint32_t legal_mask(uint32_t pitch) const {
-        uint32_t back = 8;  // direction of path[-2] from the agent, if traceback may use it
-        if constexpr (TB) {
-            if (len >= 2) back = dir_at(len - 2) ^ 2u;
-        }
+        const uint32_t back = (TB && len >= 2) ? (last ^ 2u) : 8u;  // direction of path[-2]
+        const uint32_t b = x * pitch + y;
         uint32_t m = 0;
 #pragma unroll
         for (uint32_t d = 0; d < 4; ++d) {
-            const uint32_t nx = x + dir_dx(d), ny = y + dir_dy(d);   // wraps to huge when < 0
-            const bool inb = nx < X && ny < Y;
-            const uint32_t b = inb ? nx * pitch + ny : 0u;
-            const bool ok = inb && bb_test<W>(open, b) && (!bb_test<W>(vis, b) || d == back);
+            const bool inb = d == 0 ? x + 1 < X : d == 1 ? y > 0 : d == 2 ? x > 0 : y + 1 < Y;
+            const uint32_t nb = d == 0 ? b + pitch : d == 1 ? b - 1 : d == 2 ? b - pitch : b + 1;
+            const uint32_t bb = inb ? nb : 0u;
+            const bool ok = inb && bb_test<W>(open, bb) && (!bb_test<W>(vis, bb) || d == back);
             m |= (uint32_t)ok << d;
         }
         return m;
     }
 
+    // _load_puzzle (SPaRC_Gym.py:166-187) with fresh planes; no global load on this path
+    template <class Src>
+    __device__ __forceinline__ void reset(const Src& src, uint32_t pitch, uint32_t q) {
+        uint32_t sx, sy;
+        pid = q;
+        load_puzzle(src, q, sx, sy);
+        x = sx;
+        y = sy;
+        len = 1;
+        node = 0;
+        off = (pflags & 2u) ? 0u : 1u;  // [start] is a prefix iff some solution begins at start
+        rec = src.get_root(q);          // sentinel (terminal bits 0) when there is no root
+        node_term = rec_term(rec);
+        outcome = 0;
+        pending = 0;
+        step = 0;
+        last = 0;
+#pragma unroll
+        for (int k = 0; k < W; ++k) vis[k] = 0;
+#pragma unroll
+        for (int k = 0; k < D; ++k) dirs[k] = 0;
+        bb_set<W>(vis, x * pitch + y);
+        legal = legal_mask(pitch);
+    }
+
     // one step() (SPaRC_Gym.py:1131-1223); returns reward code, writes flags
-    __device__ __forceinline__ int advance(const Params& p, uint32_t a, uint32_t& flags) {
+    template <class Src>
+    __device__ __forceinline__ int advance(const Params& p, const Src& src, uint32_t a, uint32_t& flags) {
         if (p.autoreset == 1 && pending) {   // gymnasium next-step autoreset: reset(), 1087
             const uint32_t q = pid + 1 == p.tab.num_puzzles ? 0u : pid + 1;
-            reset(p, q);
-            flags = (legal_mask(p.pitch) << 2) | 64u;
+            reset(src, p.pitch, q);
+            flags = (legal << 2) | 64u;
             return 0;
         }
-        const uint32_t legal = legal_mask(p.pitch);
         step = step < 0x7FFFFFFFu ? step + 1 : step;                     // 1132
         bool trunc = (int32_t)step >= p.max_steps;                       // 1134
         const bool moved = a < 4 && ((legal >> a) & 1u);                 // 1137
@@ -207,22 +236,25 @@ struct Env {
             if (TB && bb_test<W>(vis, b)) {                              // traceback pop 1141-1166
                 bb_clear<W>(vis, x * p.pitch + y);
                 len -= 1;
+                last = dir_at(len >= 2 ? len - 2 : 0);
                 if (off > 0) {
                     off -= 1;
                 } else {
-                    node = rec.z & 0xFFFFu;
+                    node_term = rec_parent_term(rec);
+                    node = rec_parent(rec);
                     load_rec(p);
                 }
             } else {                                                     // forward 1167-1188
                 bb_set<W>(vis, b);
                 push_dir(len - 1, a);
+                last = a;
                 len += 1;
                 if (off > 0) {
                     off += 1;
                 } else {
-                    const uint32_t cw = (a < 2) ? rec.x : rec.y;
-                    const uint32_t c = (a & 1) ? (cw >> 16) : (cw & 0xFFFFu);
+                    const uint32_t c = rec_child(rec, a);
                     if (c != kNone) {
+                        node_term = rec_child_term(rec, a);
                         node = c;
                         load_rec(p);
                     } else {
@@ -232,15 +264,14 @@ struct Env {
             }
             x = nx;
             y = ny;
+            legal = legal_mask(p.pitch);
         }
         const bool term = (x == tx) && (y == ty);                        // 1192
-        const uint32_t legal2 = legal_mask(p.pitch);
-        if (legal2 == 0) trunc = true;                                   // 1195-1196
+        if (legal == 0) trunc = true;                                    // 1195-1196
         if (term) trunc = false;                                         // 1198-1199
         int code;
         if (term || trunc) {                                             // 1204-1213
-            const bool match = off == 0 && ((rec.z >> 16) & 1u);
-            if (match) {
+            if (off == 0 && node_term) {
                 outcome = 1;
                 code = 100;
             } else if (outcome != 1) {
@@ -254,12 +285,13 @@ struct Env {
             code = (!moved || !(pflags & 1u)) ? 0 : (off == 0 ? 1 : -1);
         }
         pending = (term || trunc) ? 1u : 0u;
-        flags = (uint32_t)term | ((uint32_t)trunc << 1) | (legal2 << 2);
+        flags = (uint32_t)term | ((uint32_t)trunc << 1) | (legal << 2);
         return code;
     }
 
     // ---- SoA <-> registers
-    __device__ __forceinline__ void load(const Params& p, uint32_t i) {
+    template <class Src>
+    __device__ __forceinline__ void load(const Params& p, const Src& src, uint32_t i) {
         const State& s = p.st;
 #pragma unroll
         for (int k = 0; k < W; ++k) vis[k] = s.vis[(size_t)k * p.n + i];
@@ -277,18 +309,21 @@ struct Env {
         node = ax & 0xFFFFu;
         outcome = (ax >> 16) & 3u;
         pending = (ax >> 18) & 1u;
+        node_term = (ax >> 19) & 1u;
         step = s.step[i];
         pid = s.pid[i];
         uint32_t sx, sy;
-        load_puzzle(p, pid, sx, sy);
-        // keep the invariant: pops can bring `off` back to 0 at any later step of a launch.
-        // Puzzles whose root is not a prefix (flags bit1 clear) have off >= 1 forever and may
-        // have no trie nodes at all.
+        load_puzzle(src, pid, sx, sy);
+        // invariant: rec is node's record whenever the root is valid (pops can bring `off`
+        // back to 0 at any later step).  Rootless puzzles (flags bit1 clear) keep off >= 1.
         if (pflags & 2u) load_rec(p);
         else rec = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, kNone, 0u);
+        last = (TB && len >= 2) ? dir_at(len - 2) : 0u;
+        legal = legal_mask(p.pitch);
     }
 
-    __device__ __forceinline__ void store(const Params& p, uint32_t i) const {
+    template <class Src>
+    __device__ __forceinline__ void store(const Params& p, const Src&, uint32_t i) const {
         const State& s = p.st;
 #pragma unroll
         for (int k = 0; k < W; ++k) s.vis[(size_t)k * p.n + i] = vis[k];
@@ -297,9 +332,203 @@ struct Env {
             for (int k = 0; k < D; ++k) s.dirs[(size_t)k * p.n + i] = dirs[k];
         }
         s.pos[i] = x | (y << 8) | (len << 16) | (off << 24);
-        s.aux[i] = node | (outcome << 16) | (pending << 18);
+        s.aux[i] = node | (outcome << 16) | (pending << 18) | (node_term << 19);
         s.step[i] = step;
         s.pid[i] = pid;
+    }
+};
+
+// ---------------------------------------------------------------------------------------------
+// W = 1 specialisation: lattices that fit a 64-bit board PADDED by one blocked column
+// (pitch > y_size) and one blocked row (x_size + 1 rows), i.e. (x_size + 1) * pitch <= 64
+// (every 7x7 and 5x5 pool; the host packer picks this geometry).  The agent is the bit index
+// b = x*pitch + y; `blk` = visited | not-open is the only bitboard in registers, and the four
+// neighbour tests of _get_legal_actions are one 32-bit window of blk starting at b - pitch
+// (bits 0: left, pitch-1: up, pitch+1: down, 2*pitch: right), with no bounds compares
+// (out-of-lattice neighbours are padding = blocked; below bit 0 reads as blocked).  The step is branch-free except for the
+// autoreset and the trie-record load.
+template <bool TB>
+struct Env<1, TB> {
+    uint64_t blk;        // blocked: visited | ~open (padding and gaps included)
+    uint64_t dlo, dhi;   // direction stack, 2 bits per move (<= 63 moves on a 64-bit board)
+    uint32_t b, len, off, node, node_term, outcome, pending, step, pid, legal, last;
+    uint32_t tgt, pflags, trie_base, trie_cnt;
+    uint32_t bad = 0;    // sticky: a trie index was out of range (reported at store)
+    uint4 rec;
+
+    // all arms are computed unconditionally and merged with masks: a C++ ?: whose arms are
+    // 64-bit shifts is otherwise lowered to exec-masked if/else blocks
+    __device__ __forceinline__ static uint32_t pick(bool c, uint32_t a, uint32_t b) {
+        const uint32_t m = 0u - (uint32_t)c;
+        return (a & m) | (b & ~m);
+    }
+
+    __device__ __forceinline__ uint32_t legal_mask(uint32_t P) const {
+        // 32-bit window whose bit j is blocked(b - P + j); below bit 0 reads as blocked
+        const uint32_t sr = (b - P) & 63u, sl = (P - b) & 31u;
+        const uint32_t above = (uint32_t)(blk >> sr);
+        const uint32_t below = (uint32_t)(blk << sl) | ((1u << sl) - 1u);
+        const uint32_t w = ~pick(b >= P, above, below);                 // free bits (2P + 1 <= 31)
+        uint32_t m = ((w >> (2 * P)) & 1u) | (((w >> (P - 1)) & 1u) << 1) | ((w & 1u) << 2) |
+                     (((w >> (P + 1)) & 1u) << 3);
+        if constexpr (TB) {
+            // path[-2] is the reverse of the last move; it is open unless it is a closed start
+            const uint32_t back = (uint32_t)(len >= 3) | ((uint32_t)(len == 2) & ((~pflags >> 2) & 1u));
+            m |= back << (last ^ 2u);
+        }
+        return m;
+    }
+
+    template <class Src>
+    __device__ __forceinline__ void load_puzzle(const Src& src, uint32_t q, uint32_t P, uint32_t& sb) {
+        const uint4 inf = src.get_info(q);
+        sb = ((inf.x >> 16) & 0xFFu) * P + (inf.x >> 24);
+        tgt = (inf.y & 0xFFu) * P + ((inf.y >> 8) & 0xFFu);
+        pflags = inf.y >> 16;
+        trie_base = inf.z;
+        trie_cnt = inf.w;
+    }
+
+    // node < trie_cnt always holds (host-validated tables); a violation is recorded in `bad`
+    // (reported through the error word at the end of the launch) instead of reading out of bounds
+    __device__ __forceinline__ void load_rec(const Params& p) {
+        const bool oob = node >= trie_cnt;
+        bad |= oob ? 1u : 0u;
+        rec = p.tab.trie[trie_base + (oob ? 0u : node)];
+    }
+
+    template <class Src>
+    __device__ __forceinline__ void reset(const Src& src, uint32_t P, uint32_t q) {
+        uint32_t sb;
+        pid = q;
+        load_puzzle(src, q, P, sb);
+        b = sb;
+        blk = ~src.get_open(q, 0) | (1ull << sb);
+        len = 1;
+        node = 0;
+        off = (pflags & 2u) ? 0u : 1u;
+        rec = src.get_root(q);
+        node_term = rec_term(rec);
+        outcome = 0;
+        pending = 0;
+        step = 0;
+        last = 0;
+        dlo = dhi = 0;
+        legal = legal_mask(P);
+    }
+
+    template <class Src>
+    __device__ __forceinline__ int advance(const Params& p, const Src& src, uint32_t a, uint32_t& flags) {
+        const uint32_t P = p.pitch;
+        if (p.autoreset == 1 && pending) {
+            const uint32_t q = pid + 1 == p.tab.num_puzzles ? 0u : pid + 1;
+            reset(src, P, q);
+            flags = (legal << 2) | 64u;
+            return 0;
+        }
+        step += (uint32_t)(step < 0x7FFFFFFFu);                                     // 1132
+        const bool trunc0 = (int32_t)step >= p.max_steps;                          // 1134
+        const uint32_t ad = a & 3u;
+        const bool moved = (a < 4u) & (bool)((legal >> ad) & 1u);                  // 1137
+        // neighbour offset: right +P, up -1, left -P, down +1
+        const uint32_t mag = P - ((P - 1u) & (0u - (ad & 1u)));
+        const uint32_t neg = 0u - ((ad ^ (ad >> 1)) & 1u);
+        const uint32_t nb = b + ((mag ^ neg) - neg);
+        const bool pop = TB & moved & ((ad ^ 2u) == last) & (len >= 2);           // 1141-1166
+        const bool fwd = moved & !pop;                                             // 1167-1188
+        // visited: forward sets the new node, a pop clears the node it leaves
+        const uint32_t tog = pick(fwd, nb, b);
+        blk ^= (uint64_t)moved << (tog & 63u);   // (an illegal move's nb may be out of range)
+        if constexpr (TB) {
+            // push `a` at move index len-1, or re-read the move before the popped one
+            const uint32_t k = pick(fwd, len - 1u, len >= 3 ? len - 3u : 0u);
+            const uint32_t sh = (k & 31u) * 2u;
+            const bool hiw = k >= 32;
+            const uint64_t wsel = hiw ? dhi : dlo;
+            const uint32_t prev = (uint32_t)(wsel >> sh) & 3u;
+            const uint64_t upd = (wsel & ~(3ull << sh)) | ((uint64_t)ad << sh);
+            dlo = (fwd & !hiw) ? upd : dlo;
+            dhi = (fwd & hiw) ? upd : dhi;
+            last = pick(fwd, ad, pick(pop, prev, last));
+        }
+        len = len + (uint32_t)fwd - (uint32_t)pop;
+        // solution trie
+        const bool on = off == 0;
+        const uint32_t c = rec_child(rec, ad);
+        const bool down = fwd & on & (c != kNone);
+        const bool up = pop & on;
+        node_term = pick(down, rec_child_term(rec, ad), pick(up, rec_parent_term(rec), node_term));
+        node = pick(down, c, pick(up, rec_parent(rec), node));
+        off = pick(on, (uint32_t)(fwd & (c == kNone)), off + (uint32_t)fwd - (uint32_t)pop);
+        if (down | up) load_rec(p);
+        b = pick(moved, nb, b);
+        legal = legal_mask(P);
+        const bool term = b == tgt;                                                // 1192
+        const bool trunc = (trunc0 | (legal == 0)) & !term;                        // 1195-1199
+        const bool done = term | trunc;
+        const bool match = (off == 0) & (node_term != 0);
+        // reward code (1204-1223): done: +100 on a solution, else -100 unless the previous done
+        // step already set outcome_reward = 1 (then 0); otherwise +-1 when moved (0 if no solutions)
+        const int c_done = match ? 100 : (outcome != 1 ? -100 : 0);
+        const int c_move = (moved & (bool)(pflags & 1u)) ? (off == 0 ? 1 : -1) : 0;
+        const int code = done ? c_done : c_move;
+        outcome = pick(done, pick(match | (outcome == 1), 1u, 2u), 0u);
+        pending = (uint32_t)done;
+        flags = (uint32_t)term | ((uint32_t)trunc << 1) | (legal << 2);
+        return code;
+    }
+
+    template <class Src>
+    __device__ __forceinline__ void load(const Params& p, const Src& src, uint32_t i) {
+        const State& s = p.st;
+        const uint32_t P = p.pitch;
+        const uint64_t vis = s.vis[i];
+        if constexpr (TB) {
+            dlo = s.dirs[i];
+            dhi = s.dirs[(size_t)p.n + i];
+        } else {
+            dlo = dhi = 0;
+        }
+        const uint32_t ps = s.pos[i], ax = s.aux[i];
+        b = (ps & 0xFFu) * P + ((ps >> 8) & 0xFFu);
+        len = (ps >> 16) & 0xFFu;
+        off = ps >> 24;
+        node = ax & 0xFFFFu;
+        outcome = (ax >> 16) & 3u;
+        pending = (ax >> 18) & 1u;
+        node_term = (ax >> 19) & 1u;
+        step = s.step[i];
+        pid = s.pid[i];
+        bad = 0;
+        uint32_t sb;
+        load_puzzle(src, pid, P, sb);
+        blk = vis | ~src.get_open(pid, 0);
+        if (pflags & 2u) load_rec(p);
+        else rec = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, kNone, 0u);
+        if constexpr (TB) {
+            const uint32_t k = len >= 2 ? len - 2 : 0u;
+            last = (uint32_t)((k < 32 ? dlo : dhi) >> ((k & 31u) * 2u)) & 3u;
+        } else {
+            last = 0;
+        }
+        legal = legal_mask(P);
+    }
+
+    template <class Src>
+    __device__ __forceinline__ void store(const Params& p, const Src& src, uint32_t i) const {
+        const State& s = p.st;
+        const uint32_t P = p.pitch;
+        s.vis[i] = blk & src.get_open(pid, 0);
+        if constexpr (TB) {
+            s.dirs[i] = dlo;
+            s.dirs[(size_t)p.n + i] = dhi;
+        }
+        const uint32_t x = b / P, y = b - x * P;
+        s.pos[i] = x | (y << 8) | (len << 16) | (off << 24);
+        s.aux[i] = node | (outcome << 16) | (pending << 18) | (node_term << 19);
+        s.step[i] = step;
+        s.pid[i] = pid;
+        if (bad) atomicOr(p.err, (int)kErrTrie);
     }
 };
 

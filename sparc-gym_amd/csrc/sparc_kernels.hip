@@ -10,6 +10,7 @@
 // No MFMA: this is integer / bitboard work, bound by latency and HBM.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -24,7 +25,15 @@ using namespace sparc;
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kChunk = 8;   // actions prefetched per lane in k_rollout
+constexpr int kTile = 16;                             // env-steps per LDS-transposed I/O tile
+constexpr int kTileBytes = 3 * 64 * kTile;            // per wave: actions, reward codes, flags
+constexpr int kTilesLds = (kBlock / 64) * kTileBytes;  // 12 KiB per workgroup
+constexpr size_t kMaxDynLds = 64 * 1024;
+
+template <int W>
+__host__ __device__ constexpr size_t table_lds_bytes(uint32_t P) {
+    return (size_t)P * (2 * sizeof(uint4) + W * sizeof(uint64_t));
+}
 
 template <int W, bool TB>
 __global__ void __launch_bounds__(kBlock) k_reset(Params p, const uint32_t* __restrict__ q,
@@ -34,13 +43,14 @@ __global__ void __launch_bounds__(kBlock) k_reset(Params p, const uint32_t* __re
     if (mask && !mask[i]) return;
     const uint32_t pid = q[i];
     if (pid >= p.tab.num_puzzles) {
-        atomicOr(p.err, 1);
+        atomicOr(p.err, (int)kErrPuzzle);
         return;
     }
+    const PuzzleSrc<W> src{p.tab.info, p.tab.root, p.tab.open};
     Env<W, TB> e;
-    e.reset(p, pid);
-    e.store(p, i);
-    if (flg) flg[i] = (uint8_t)(e.legal_mask(p.pitch) << 2);
+    e.reset(src, p.pitch, pid);
+    e.store(p, src, i);
+    if (flg) flg[i] = (uint8_t)(e.legal << 2);
 }
 
 template <int W, bool TB>
@@ -48,60 +58,121 @@ __global__ void __launch_bounds__(kBlock) k_step(Params p, const uint8_t* __rest
                                                  int8_t* __restrict__ rew, uint8_t* __restrict__ flg) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= p.n) return;
+    const PuzzleSrc<W> src{p.tab.info, p.tab.root, p.tab.open};
     Env<W, TB> e;
-    e.load(p, i);
+    e.load(p, src, i);
     uint32_t f;
-    const int c = e.advance(p, act[i], f);
-    e.store(p, i);
+    const int c = e.advance(p, src, act[i], f);
+    e.store(p, src, i);
     rew[i] = (int8_t)c;
     flg[i] = (uint8_t)f;
 }
 
-template <int W, bool TB, bool RAND>
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// streamed-once I/O: nontemporal so that actions / outputs do not evict the trie from L2
+__device__ __forceinline__ u32x4 nt_load16(const uint8_t* q) {
+    return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(q));
+}
+__device__ __forceinline__ void nt_store16(uint8_t* q, u32x4 v) {
+    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(q));
+}
+
+// orders one wave's LDS accesses across its lanes (a wave's DS instructions execute in order;
+// this only stops the compiler from moving them)
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// T steps per env with the state in VGPRs.  Full waves with `tiled` (16-B aligned I/O, n % 16
+// == 0) move actions / reward codes / flags in [16 steps][64 envs] tiles: one dwordx4 load and
+// two dwordx4 stores per lane per 16 steps, transposed through a per-wave LDS tile, the next
+// action tile prefetched one tile ahead.  Other waves / the tail use per-step byte accesses.
+// With LDS_TABLE the puzzle rows (info, root record, open bitboard) are staged in LDS once, so
+// autoresets issue no global load; the only global reads in the loop are trie records, issued
+// at on-trie transitions and first consumed at the next one.
+template <int W, bool TB, bool RAND, bool LDS_TABLE>
 __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const uint8_t* __restrict__ act,
                                                     uint64_t seed, uint64_t t0, int8_t* __restrict__ rew,
-                                                    uint8_t* __restrict__ flg, int4* __restrict__ stats) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= p.n) return;
-    Env<W, TB> e;
-    e.load(p, i);
+                                                    uint8_t* __restrict__ flg, int4* __restrict__ stats,
+                                                    uint32_t tiled) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint8_t* ta = smem + wv * kTileBytes;
+    uint8_t* tr = ta + 64 * kTile;
+    uint8_t* tf = tr + 64 * kTile;
+    PuzzleSrc<W> src{p.tab.info, p.tab.root, p.tab.open};
+    if constexpr (LDS_TABLE) {
+        const uint32_t P = p.tab.num_puzzles;
+        uint4* linfo = reinterpret_cast<uint4*>(smem + kTilesLds);
+        uint4* lroot = linfo + P;
+        uint64_t* lopen = reinterpret_cast<uint64_t*>(lroot + P);
+        for (uint32_t k = threadIdx.x; k < P; k += kBlock) {
+            linfo[k] = p.tab.info[k];
+            lroot[k] = p.tab.root[k];
+        }
+        for (uint32_t k = threadIdx.x; k < P * W; k += kBlock) lopen[k] = p.tab.open[k];
+        __syncthreads();
+        src = PuzzleSrc<W>{linfo, lroot, lopen};
+    }
+    const uint32_t wave_base = blockIdx.x * kBlock + wv * 64;
+    if (wave_base >= p.n) return;
+    const uint32_t i = wave_base + lane;
+    const bool active = i < p.n;
+    const bool full = tiled && wave_base + 64 <= p.n;   // wave-uniform
     const size_t n = p.n;
     const uint64_t gid = p.env_offset + i;
+    const uint32_t r = lane >> 2, c = (lane & 3) * 16;   // this lane's 16-byte piece of a tile
+    Env<W, TB> e;
+    if (active) e.load(p, src, i);
     int4 acc = make_int4(0, 0, 0, 0);
-    uint32_t cur[kChunk], nxt[kChunk];
-    if constexpr (!RAND) {
-#pragma unroll
-        for (int k = 0; k < kChunk; ++k) cur[k] = k < T ? act[(size_t)k * n + i] : 0u;
-    }
-    for (int32_t tc = 0; tc < T; tc += kChunk) {
-        if constexpr (!RAND) {   // prefetch the next chunk while this one is stepped
-#pragma unroll
-            for (int k = 0; k < kChunk; ++k) {
-                const int32_t t = tc + kChunk + k;
-                nxt[k] = t < T ? act[(size_t)t * n + i] : 0u;
+    u32x4 anext = {0u, 0u, 0u, 0u};
+    if (!RAND && full && T >= kTile) anext = nt_load16(act + (size_t)r * n + wave_base + c);
+
+    for (int32_t tb = 0; tb < T; tb += kTile) {
+        const int32_t cnt = T - tb < kTile ? T - tb : kTile;
+        if (full && cnt == kTile) {
+            if constexpr (!RAND) {
+                const u32x4 acur = anext;
+                if (tb + 2 * kTile <= T) anext = nt_load16(act + (size_t)(tb + kTile + r) * n + wave_base + c);
+                *reinterpret_cast<u32x4*>(ta + r * 64 + c) = acur;
+                wave_lds_fence();
             }
-        }
-#pragma unroll
-        for (int k = 0; k < kChunk; ++k) {
-            const int32_t t = tc + k;
-            if (t < T) {
-                const uint32_t a = RAND ? uint_rand_action(seed, gid, t0 + (uint64_t)t) : cur[k];
+#pragma unroll 4
+            for (int k = 0; k < kTile; ++k) {
+                const uint32_t a = RAND ? uint_rand_action(seed, gid, t0 + (uint64_t)(tb + k)) : ta[k * 64 + lane];
                 uint32_t f;
-                const int c = e.advance(p, a, f);
-                if (rew) rew[(size_t)t * n + i] = (int8_t)c;
-                if (flg) flg[(size_t)t * n + i] = (uint8_t)f;
-                acc.x += c;
+                const int code = e.advance(p, src, a, f);
+                tr[k * 64 + lane] = (uint8_t)code;
+                tf[k * 64 + lane] = (uint8_t)f;
+                acc.x += code;
                 acc.y += (f & 3u) ? 1 : 0;
-                acc.z += ((f & 3u) && c == 100) ? 1 : 0;
+                acc.z += ((f & 3u) && code == 100) ? 1 : 0;
+                acc.w += (f & 64u) ? 1 : 0;
+            }
+            wave_lds_fence();
+            const size_t o = (size_t)(tb + r) * n + wave_base + c;
+            if (rew) nt_store16(reinterpret_cast<uint8_t*>(rew) + o, *reinterpret_cast<const u32x4*>(tr + r * 64 + c));
+            if (flg) nt_store16(flg + o, *reinterpret_cast<const u32x4*>(tf + r * 64 + c));
+            wave_lds_fence();
+        } else if (active) {
+            for (int k = 0; k < cnt; ++k) {
+                const int32_t t = tb + k;
+                const uint32_t a = RAND ? uint_rand_action(seed, gid, t0 + (uint64_t)t) : act[(size_t)t * n + i];
+                uint32_t f;
+                const int code = e.advance(p, src, a, f);
+                if (rew) rew[(size_t)t * n + i] = (int8_t)code;
+                if (flg) flg[(size_t)t * n + i] = (uint8_t)f;
+                acc.x += code;
+                acc.y += (f & 3u) ? 1 : 0;
+                acc.z += ((f & 3u) && code == 100) ? 1 : 0;
                 acc.w += (f & 64u) ? 1 : 0;
             }
         }
-        if constexpr (!RAND) {
-#pragma unroll
-            for (int k = 0; k < kChunk; ++k) cur[k] = nxt[k];
-        }
     }
-    e.store(p, i);
+    if (!active) return;
+    e.store(p, src, i);
     if (stats) {
         int4 s = stats[i];
         s.x += acc.x;
@@ -144,7 +215,7 @@ struct Ctx {
     uint64_t *vis = nullptr, *dirs = nullptr;
     uint32_t *pos = nullptr, *aux = nullptr, *step = nullptr, *pid = nullptr;
     uint64_t* t_open = nullptr;
-    uint4 *t_info = nullptr, *t_trie = nullptr;
+    uint4 *t_info = nullptr, *t_root = nullptr, *t_trie = nullptr;
     int32_t* err = nullptr;
     uint8_t *s_act = nullptr, *s_flags = nullptr, *s_mask = nullptr;
     int8_t* s_rew = nullptr;
@@ -171,6 +242,7 @@ Params make_params(const Ctx* c) {
     Params p{};
     p.tab.open = c->t_open;
     p.tab.info = c->t_info;
+    p.tab.root = c->t_root;
     p.tab.trie = c->t_trie;
     p.tab.num_puzzles = c->num_puzzles;
     p.st.vis = c->vis;
@@ -274,7 +346,7 @@ int sparc_destroy(void* ctx) {
     if (!c) return SPARC_OK;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void* bufs[] = {c->vis, c->dirs, c->pos, c->aux, c->step, c->pid, c->t_open, c->t_info, c->t_trie,
+    void* bufs[] = {c->vis, c->dirs, c->pos, c->aux, c->step, c->pid, c->t_open, c->t_info, c->t_root, c->t_trie,
                     c->err, c->s_act, c->s_flags, c->s_mask, c->s_rew, c->s_pidx};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -327,8 +399,11 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
         const uint32_t tx = inf[1] & 0xFF, ty = (inf[1] >> 8) & 0xFF, fl = inf[1] >> 16;
         const uint32_t base = inf[2], cnt = inf[3];
         char m[160];
-        if (X < 1 || Y < 1 || Y > pitch || (X - 1) * pitch + Y > 64u * W) {
-            snprintf(m, sizeof m, "puzzle %d: lattice %ux%u does not fit pitch %u / %d words", q, X, Y, pitch, W);
+        const bool fits = W == 1 ? (Y < pitch && pitch <= 15 && (X + 1) * pitch <= 64u)
+                                 : (Y <= pitch && (X - 1) * pitch + Y <= 64u * W);
+        if (X < 1 || Y < 1 || !fits) {
+            snprintf(m, sizeof m, "puzzle %d: lattice %ux%u does not fit pitch %u / %d words%s", q, X, Y, pitch, W,
+                     W == 1 ? " (words=1 needs the padded layout)" : "");
             return fail(c, SPARC_E_INVALID, m);
         }
         if (sx >= X || sy >= Y || tx >= X || ty >= Y) {
@@ -355,13 +430,26 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
     if (c->t_open) HIPCHK(c, hipFree(c->t_open));
     if (c->t_info) HIPCHK(c, hipFree(c->t_info));
     if (c->t_trie) HIPCHK(c, hipFree(c->t_trie));
+    if (c->t_root) HIPCHK(c, hipFree(c->t_root));
     c->t_open = nullptr;
     c->t_info = nullptr;
+    c->t_root = nullptr;
     c->t_trie = nullptr;
     const size_t P = (size_t)t->num_puzzles, nn = (size_t)(t->num_nodes > 0 ? t->num_nodes : 1);
     HIPCHK(c, hipMalloc(&c->t_open, sizeof(uint64_t) * P * W));
     HIPCHK(c, hipMalloc(&c->t_info, sizeof(uint4) * P));
     HIPCHK(c, hipMalloc(&c->t_trie, sizeof(uint4) * nn));
+    HIPCHK(c, hipMalloc(&c->t_root, sizeof(uint4) * P));
+    // each puzzle's root record, so that a reset needs no dependent trie load
+    std::vector<uint4> roots(P, make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, kNone, 0u));
+    for (size_t q = 0; q < P; ++q) {
+        const uint32_t* inf = t->info + 4 * q;
+        if ((inf[1] >> 16) & 2u) {
+            const uint32_t* r = t->trie + 4 * (size_t)inf[2];
+            roots[q] = make_uint4(r[0], r[1], r[2], r[3]);
+        }
+    }
+    HIPCHK(c, hipMemcpy(c->t_root, roots.data(), sizeof(uint4) * P, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->t_open, t->open, sizeof(uint64_t) * P * W, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->t_info, t->info, sizeof(uint4) * P, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemset(c->t_trie, 0xFF, sizeof(uint4) * nn));
@@ -441,13 +529,31 @@ int sparc_rollout_device(void* ctx, int32_t T, const uint8_t* d_act, uint64_t se
     if ((uint64_t)T * c->n > (1ull << 40)) return fail(c, SPARC_E_INVALID, "T*N too large");
     const Params p = make_params(c);
     int4* st = reinterpret_cast<int4*>(d_stats);
+    auto aligned = [](const void* q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & 15u) == 0; };
+    const uint32_t tiled = (c->n % 16 == 0) && aligned(d_act) && aligned(d_rew) && aligned(d_flags);
+    // stage the puzzle rows in LDS when they fit next to the I/O tiles without costing
+    // occupancy: budget = LDS per CU / resident workgroups per CU (256 CUs)
+    const size_t blocks = (c->n + kBlock - 1) / kBlock;
+    const size_t per_cu = (blocks + 255) / 256;
+    const size_t budget = std::min(kMaxDynLds, (size_t)160 * 1024 / (per_cu ? per_cu : 1));
     dispatch_w_tb(c->W, c->cfg.traceback, [&](auto w, auto tb) {
         constexpr int W = decltype(w)::value;
         constexpr bool TB = decltype(tb)::value;
-        if (d_act)
-            k_rollout<W, TB, false><<<grid_for(c->n), kBlock, 0, c->stream>>>(p, T, d_act, seed, t0, d_rew, d_flags, st);
-        else
-            k_rollout<W, TB, true><<<grid_for(c->n), kBlock, 0, c->stream>>>(p, T, nullptr, seed, t0, d_rew, d_flags, st);
+        const size_t tbytes = table_lds_bytes<W>(c->num_puzzles);
+        const bool lds_table = kTilesLds + tbytes <= budget;
+        const size_t shm = kTilesLds + (lds_table ? tbytes : 0);
+        const dim3 g = grid_for(c->n);
+        if (d_act) {
+            if (lds_table)
+                k_rollout<W, TB, false, true><<<g, kBlock, shm, c->stream>>>(p, T, d_act, seed, t0, d_rew, d_flags, st, tiled);
+            else
+                k_rollout<W, TB, false, false><<<g, kBlock, shm, c->stream>>>(p, T, d_act, seed, t0, d_rew, d_flags, st, tiled);
+        } else {
+            if (lds_table)
+                k_rollout<W, TB, true, true><<<g, kBlock, shm, c->stream>>>(p, T, nullptr, seed, t0, d_rew, d_flags, st, tiled);
+            else
+                k_rollout<W, TB, true, false><<<g, kBlock, shm, c->stream>>>(p, T, nullptr, seed, t0, d_rew, d_flags, st, tiled);
+        }
     });
     return launch_check(c);
 }

@@ -151,17 +151,36 @@ class PuzzleTable:
 
 
 def lattice_geometry(puzzles, pitch=None, words=None):
+    """Bitboard geometry (pitch, words, x_max, y_max) for a pool.
+
+    words == 1 is the PADDED 64-bit layout of the kernel's fast path: pitch > y_max (a blocked
+    column) and (x_max + 1) * pitch <= 64 (a blocked row), pitch <= 15 — every 7x7 or 5x5
+    pool.  Larger lattices use 2 or 4 words with pitch >= y_max and explicit bounds checks.
+    """
     x_max = max(int(p["x_size"]) for p in puzzles)
     y_max = max(int(p["y_size"]) for p in puzzles)
-    pitch = y_max if pitch is None else int(pitch)
+    if x_max > 255 or y_max > 255:
+        raise ValueError("lattice too large")
+    padded_ok = lambda pt: y_max < pt <= 15 and (x_max + 1) * pt <= 64  # noqa: E731
+    if words is None:
+        if pitch is None and padded_ok(y_max + 1):
+            return y_max + 1, 1, x_max, y_max
+        if pitch is not None and padded_ok(int(pitch)):
+            return int(pitch), 1, x_max, y_max
+    pitch = (y_max + 1 if words == 1 else y_max) if pitch is None else int(pitch)
     if pitch < y_max:
         raise ValueError(f"pitch {pitch} < max y_size {y_max}")
+    if words == 1:
+        if not padded_ok(pitch):
+            raise ValueError(f"words=1 needs a padded geometry: {y_max} < pitch <= 15 and "
+                             f"(x_max + 1) * pitch <= 64 (x_max={x_max}, pitch={pitch})")
+        return pitch, 1, x_max, y_max
     bits = (x_max - 1) * pitch + y_max
-    need = 1 if bits <= 64 else 2 if bits <= 128 else 4 if bits <= 256 else None
-    if need is None or x_max > 255:
+    need = 2 if bits <= 128 else 4 if bits <= 256 else None
+    if need is None:
         raise ValueError(f"lattice {x_max}x{y_max} exceeds the 256-bit bitboard (15x15 lattices max)")
     words = need if words is None else int(words)
-    if words not in (1, 2, 4) or words < need:
+    if words not in (2, 4) or words < need:
         raise ValueError(f"words={words} cannot hold a {x_max}x{pitch} lattice")
     return pitch, words, x_max, y_max
 
@@ -234,16 +253,26 @@ def pack_table(puzzles, pitch=None, words=None):
             # the reference raises IndexError lazily at SPaRC_Gym.py:1206/1218; refuse up front
             raise ValueError(f"puzzle {q}: solution_count {nsol} > {len(sols)} stored solutions")
         nodes, root_valid = build_trie((sx, sy), sols[:max(nsol, 0)])
-        flags = (1 if nsol > 0 else 0) | (2 if root_valid else 0)
+        start_closed = gaps[sx, sy] != 0
+        flags = (1 if nsol > 0 else 0) | (2 if root_valid else 0) | (4 if start_closed else 0)
         info[q, 0] = X | (Y << 8) | (sx << 16) | (sy << 24)
         info[q, 1] = tx | (ty << 8) | (flags << 16)
         if root_valid:
             info[q, 2], info[q, 3] = base, len(nodes)
-            arr = np.asarray(nodes, np.uint32)
+            arr = np.asarray(nodes, np.int64)
+            term = arr[:, 5]
+            # terminal bits of the 4 children and of the parent, so that the kernel knows a
+            # new node's terminal flag without waiting for that node's record
+            kid_term = np.zeros(len(nodes), np.int64)
+            for d in range(4):
+                has = arr[:, d] != _NONE
+                kid_term |= np.where(has, term[np.where(has, arr[:, d], 0)], 0) << d
+            par = arr[:, 4]
+            par_term = np.where(par != _NONE, term[np.where(par != _NONE, par, 0)], 0)
             rec = np.zeros((len(nodes), 4), np.uint32)
             rec[:, 0] = arr[:, 0] | (arr[:, 1] << 16)
             rec[:, 1] = arr[:, 2] | (arr[:, 3] << 16)
-            rec[:, 2] = arr[:, 4] | (arr[:, 5] << 16)
+            rec[:, 2] = par | (term << 16) | (kid_term << 17) | (par_term << 21)
             rec[:, 3] = arr[:, 6]
             tries.append(rec)
             base += len(nodes)

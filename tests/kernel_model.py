@@ -1,7 +1,8 @@
 """Line-by-line Python model of sparc-gym_amd/csrc/sparc_env.hpp + k_rollout (TEST ONLY).
 
 It executes the device algorithm (bitboards, 2-bit direction stack, trie node + off-trie depth,
-the `rec` register and its invariant, per-launch SoA load/store with the same bit packing) on
+the `rec` register and its invariant, node_term from the parent's child-terminal bits,
+the carried legal mask, per-launch SoA load/store with the same bit packing) on
 the host, so design errors in the kernel logic show up in the CPU suite instead of as GPU
 faults.  It reads the packed PuzzleTable exactly as the kernel does, including the bounds
 guard on trie indices (which must never fire).
@@ -45,19 +46,26 @@ class KernelModel:
             e["node"] = 0
         e["rec"] = tuple(int(v) for v in self.t.trie[e["trie_base"] + e["node"]])
 
+    def _root(self, e, q):
+        if e["pflags"] & 2:
+            return tuple(int(v) for v in self.t.trie[e["trie_base"]])
+        return SENTINEL
+
     def _reset(self, e, q):
         sx, sy = self._puzzle(e, q)
         e.update(pid=q, x=sx, y=sy, len=1, node=0, off=0 if e["pflags"] & 2 else 1, outcome=0,
-                 pending=0, step=0, dirs=0, vis=1 << (sx * self.t.pitch + sy))
-        if e["off"] == 0:
-            self._load_rec(e)
-        else:
-            e["rec"] = SENTINEL
+                 pending=0, step=0, dirs=0, last=0, vis=1 << (sx * self.t.pitch + sy))
+        e["rec"] = self._root(e, q)
+        e["node_term"] = (e["rec"][2] >> 16) & 1
+        e["legal"] = self._legal(e)
+
+    def _dir_at(self, e, k):
+        return (e["dirs"] >> (2 * k)) & 3
 
     def _legal(self, e):
-        back = 8
-        if self.tb and e["len"] >= 2:
-            back = ((e["dirs"] >> (2 * (e["len"] - 2))) & 3) ^ 2
+        if self.t.words == 1:
+            return self._legal_w1(e)
+        back = (e["last"] ^ 2) if (self.tb and e["len"] >= 2) else 8
         m = 0
         for d in range(4):
             nx, ny = e["x"] + DX[d], e["y"] + DY[d]
@@ -68,30 +76,52 @@ class KernelModel:
                 m |= 1 << d
         return m
 
+    def _legal_w1(self, e):
+        """Env<1, TB>::legal_mask: one window over the padded 64-bit blocked board."""
+        P, M = self.t.pitch, (1 << 64) - 1
+        b = e["x"] * P + e["y"]
+        blk = (e["vis"] | (~e["open"] & M)) & M
+        if b >= P:
+            win = (blk >> (b - P)) & 0xFFFFFFFF
+        else:
+            win = ((blk << (P - b)) & 0xFFFFFFFF) | ((1 << (P - b)) - 1)
+        w = ~win & 0xFFFFFFFF
+        m = ((w >> (2 * P)) & 1) | (((w >> (P - 1)) & 1) << 1) | ((w & 1) << 2) | (((w >> (P + 1)) & 1) << 3)
+        if self.tb and (e["len"] >= 3 or (e["len"] == 2 and not e["pflags"] & 4)):
+            m |= 1 << (e["last"] ^ 2)
+        return m
+
     def _advance(self, e, a):
         if self.autoreset == 1 and e["pending"]:
             q = 0 if e["pid"] + 1 == self.t.num_puzzles else e["pid"] + 1
             self._reset(e, q)
-            return 0, (self._legal(e) << 2) | 64
-        legal = self._legal(e)
+            return 0, (e["legal"] << 2) | 64
+        legal = e["legal"]
         e["step"] = e["step"] + 1 if e["step"] < 0x7FFFFFFF else e["step"]
         trunc = e["step"] >= self.max_steps
         moved = a < 4 and (legal >> a) & 1
         if moved:
             nx, ny = e["x"] + DX[a], e["y"] + DY[a]
             b = nx * self.t.pitch + ny
-            if self.tb and (e["vis"] >> b) & 1:
+            if self.t.words == 1:
+                is_pop = self.tb and (a ^ 2) == e["last"] and e["len"] >= 2
+            else:
+                is_pop = self.tb and (e["vis"] >> b) & 1
+            if is_pop:
                 e["vis"] &= ~(1 << (e["x"] * self.t.pitch + e["y"]))
                 e["len"] -= 1
+                e["last"] = self._dir_at(e, e["len"] - 2 if e["len"] >= 2 else 0)
                 if e["off"] > 0:
                     e["off"] -= 1
                 else:
+                    e["node_term"] = (e["rec"][2] >> 21) & 1
                     e["node"] = e["rec"][2] & 0xFFFF
                     self._load_rec(e)
             else:
                 e["vis"] |= 1 << b
                 k = e["len"] - 1
                 e["dirs"] = (e["dirs"] & ~(3 << (2 * k))) | (a << (2 * k))
+                e["last"] = a
                 e["len"] += 1
                 if e["off"] > 0:
                     e["off"] += 1
@@ -99,19 +129,21 @@ class KernelModel:
                     cw = e["rec"][0] if a < 2 else e["rec"][1]
                     c = (cw >> 16) if a & 1 else (cw & 0xFFFF)
                     if c != NONE:
+                        e["node_term"] = (e["rec"][2] >> (17 + a)) & 1
                         e["node"] = c
                         self._load_rec(e)
                     else:
                         e["off"] = 1
             e["x"], e["y"] = nx, ny
+            e["legal"] = self._legal(e)
         term = e["x"] == e["tx"] and e["y"] == e["ty"]
-        legal2 = self._legal(e)
+        legal2 = e["legal"]
         if legal2 == 0:
             trunc = True
         if term:
             trunc = False
         if term or trunc:
-            if e["off"] == 0 and (e["rec"][2] >> 16) & 1:
+            if e["off"] == 0 and e["node_term"]:
                 e["outcome"], code = 1, 100
             elif e["outcome"] != 1:
                 e["outcome"], code = 2, -100
@@ -130,13 +162,15 @@ class KernelModel:
              "dirs": int(sum(int(self.dirs[k, i]) << (64 * k) for k in range(2 * W))) if self.tb else 0}
         ps, ax = int(self.pos[i]), int(self.aux[i])
         e.update(x=ps & 0xFF, y=(ps >> 8) & 0xFF, len=(ps >> 16) & 0xFF, off=ps >> 24,
-                 node=ax & 0xFFFF, outcome=(ax >> 16) & 3, pending=(ax >> 18) & 1,
+                 node=ax & 0xFFFF, outcome=(ax >> 16) & 3, pending=(ax >> 18) & 1, node_term=(ax >> 19) & 1,
                  step=int(self.step_[i]), pid=int(self.pid[i]))
         self._puzzle(e, e["pid"])
         if e["pflags"] & 2:
             self._load_rec(e)
         else:
             e["rec"] = SENTINEL
+        e["last"] = self._dir_at(e, e["len"] - 2) if (self.tb and e["len"] >= 2) else 0
+        e["legal"] = self._legal(e)
         return e
 
     def _store(self, i, e):
@@ -147,7 +181,7 @@ class KernelModel:
             for k in range(2 * W):
                 self.dirs[k, i] = (e["dirs"] >> (64 * k)) & (2**64 - 1)
         self.pos[i] = e["x"] | (e["y"] << 8) | (e["len"] << 16) | (e["off"] << 24)
-        self.aux[i] = e["node"] | (e["outcome"] << 16) | (e["pending"] << 18)
+        self.aux[i] = e["node"] | (e["outcome"] << 16) | (e["pending"] << 18) | (e["node_term"] << 19)
         self.step_[i] = e["step"]
         self.pid[i] = e["pid"]
 

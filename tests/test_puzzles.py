@@ -112,9 +112,15 @@ def test_pack_table_layout():
 
 
 def test_geometry_limits():
-    assert lattice_geometry([{"x_size": 7, "y_size": 7}]) == (7, 1, 7, 7)
+    assert lattice_geometry([{"x_size": 7, "y_size": 7}]) == (8, 1, 7, 7)      # padded
+    assert lattice_geometry([{"x_size": 5, "y_size": 5}]) == (6, 1, 5, 5)
+    assert lattice_geometry([{"x_size": 7, "y_size": 7}], words=2) == (7, 2, 7, 7)
+    assert lattice_geometry([{"x_size": 7, "y_size": 9}]) == (9, 2, 7, 9)
+    assert lattice_geometry([{"x_size": 11, "y_size": 11}]) == (11, 2, 11, 11)
     assert lattice_geometry([{"x_size": 15, "y_size": 15}]) == (15, 4, 15, 15)
     with pytest.raises(ValueError):
         lattice_geometry([{"x_size": 17, "y_size": 17}])
     with pytest.raises(ValueError):
-        lattice_geometry([{"x_size": 7, "y_size": 7}], words=1, pitch=11)
+        lattice_geometry([{"x_size": 7, "y_size": 7}], words=1, pitch=7)
+    with pytest.raises(ValueError):
+        lattice_geometry([{"x_size": 9, "y_size": 9}], words=1)
