@@ -1,0 +1,38 @@
+#!/usr/bin/env python3
+"""Fixed rollout workload for rocprofv3 counter passes (same setup as bench.py's default line):
+65,536 envs, config c3, `--launches` rollout launches of `--chunk` env-steps each."""
+import argparse
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "sparc-gym_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from sparc_gym_amd import SPaRCVecEnv, synthetic  # noqa: E402
+from sparc_gym_amd.puzzles import pack_table, process_puzzles  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="c3")
+ap.add_argument("--envs", type=int, default=65536)
+ap.add_argument("--chunk", type=int, default=500)
+ap.add_argument("--launches", type=int, default=4)
+a = ap.parse_args()
+sizes, full, tb = bench.CONFIGS[a.config]
+proc = process_puzzles(synthetic.make_puzzles(1024, seed=0, sizes=sizes, full_properties=full))
+table = pack_table(proc)
+vec = SPaRCVecEnv(a.envs, processed=proc, table=table, traceback=tb, observation="compact")
+gid = np.arange(a.envs, dtype=np.uint64)
+vec.reset(options={"puzzle_index": (gid * 2654435761 % len(proc)).astype(np.int64)})
+acts = torch.randint(0, 4, (a.launches + 1, a.chunk, a.envs), dtype=torch.uint8, device="cuda")
+rew = torch.empty((a.chunk, a.envs), dtype=torch.int8, device="cuda")
+flg = torch.empty((a.chunk, a.envs), dtype=torch.uint8, device="cuda")
+stats = torch.zeros((a.envs, 4), dtype=torch.int32, device="cuda")
+for k in range(a.launches + 1):      # first launch = warmup
+    vec.rollout(a.chunk, acts[k], stats=stats, out=(rew, flg))
+torch.cuda.synchronize()
+print("done", a.config, a.envs, a.chunk, a.launches)
