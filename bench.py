@@ -115,24 +115,20 @@ def main():
     import torch
     import torch.distributed as dist
     from sparc_gym_amd import SPaRCVecEnv, synthetic
+    from sparc_gym_amd import dist as sdist
     from sparc_gym_amd.puzzles import pack_table, process_puzzles
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    rank, world, local = sdist.init_from_env("nccl")
     dev = torch.device("cuda", local)
 
     sizes, full, tb = CONFIGS[args.config]
     recs = synthetic.make_puzzles(args.puzzles, seed=0, sizes=sizes, full_properties=full)
     proc = process_puzzles(recs)
     table = pack_table(proc)
-    n = args.envs
+    offset, n = sdist.env_shard(args.envs, rank)
     vec = SPaRCVecEnv(n, processed=proc, table=table, traceback=tb, max_steps=args.max_steps,
-                      autoreset="next_step", device=local, env_offset=rank * n, observation="compact")
-    gid = np.arange(rank * n, (rank + 1) * n, dtype=np.uint64)
+                      autoreset="next_step", device=local, env_offset=offset, observation="compact")
+    gid = np.arange(offset, offset + n, dtype=np.uint64)
     vec.reset(options={"puzzle_index": (gid * 2654435761 % len(proc)).astype(np.int64)})
 
     K, W = args.steps, args.warmup
@@ -144,7 +140,6 @@ def main():
     rew = torch.empty((K, n), dtype=torch.int8, device=dev)
     flags = torch.empty((K, n), dtype=torch.uint8, device=dev)
     stats = torch.zeros((n, 4), dtype=torch.int32, device=dev)
-    gathered = torch.empty((world * n, 4), dtype=torch.int32, device=dev) if world > 1 else None
     stream = torch.cuda.current_stream(dev)
 
     def run(lo, hi, acts, rew_out, flag_out, events=None):
@@ -183,21 +178,14 @@ def main():
     events = []
     t0 = time.perf_counter()
     run(0, K, actions, rew, flags, events)
-    # end-of-batch gather of per-env summaries (reward sum, dones, solved, resets) to every rank
-    if world > 1:
-        dist.all_gather_into_tensor(gathered, stats)
+    # end-of-batch gather of per-env summaries (reward sum, dones, solved, resets): one RCCL call
+    gathered = sdist.gather_stats(stats)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if world > 1:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
-        summary = gathered.to(torch.int64).sum(0).cpu().numpy()
-    else:
-        summary = stats.to(torch.int64).sum(0).cpu().numpy()
+    elapsed = sdist.max_over_ranks(t1 - t0, dev)
+    summary = sdist.summarize(gathered)
 
     kern_ms = [a.elapsed_time(b) for (a, b), _ in events]
     steps_per_launch = [c for _, c in events]
@@ -238,8 +226,7 @@ def main():
                      "bytes_model": f"per env-step 3 B (action, reward code, flags); per env per launch "
                                     f"{per_env_launch} B (state {sb} B load+store"
                                     f"{', stats 16 B load+store' if args.mode == 'rollout' else ''})"},
-        "episodes": {"done": int(summary[1]), "solved": int(summary[2]), "autoresets": int(summary[3]),
-                     "reward_code_sum": int(summary[0])},
+        "episodes": summary,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline(proc, tb, args.max_steps, args.cpu_seconds)

@@ -1,0 +1,61 @@
+"""Multi-GPU data parallelism over independent env shards.
+
+The reference is one env per process (SPaRC_Gym.py:44; llm_host.py:257-264 runs independent
+envs concurrently).  Here each rank (one process per GPU) owns a contiguous range of global env
+ids, steps it with no communication, and at the end of a rollout batch the per-env summaries
+(reward-code sum, done steps, solved steps, autoresets: the ``stats`` [N, 4] int32 of
+``SPaRCVecEnv.rollout``) are gathered with ONE all_gather (RCCL over xGMI with backend "nccl";
+gloo in the CPU tests).  Global env id = rank * envs_per_rank + local id, which also seeds the
+counter-based random actions, so a sharded run reproduces the single-process run of all envs.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def env_shard(envs_per_rank: int, rank: int):
+    """(env_offset, count) of this rank's contiguous shard (weak scaling: fixed per rank)."""
+    return rank * envs_per_rank, envs_per_rank
+
+
+def init_from_env(backend="nccl"):
+    """Initialise torch.distributed from torchrun's environment; returns (rank, world, local)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    return rank, world, local
+
+
+def gather_stats(stats: torch.Tensor, group=None) -> torch.Tensor:
+    """End-of-batch gather: [N, 4] int32 per rank -> [world * N, 4] on every rank, ordered by
+    global env id.  A single all_gather (one RCCL call per batch, never per step)."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return stats
+    world = dist.get_world_size(group)
+    out = torch.empty((world * stats.shape[0],) + tuple(stats.shape[1:]), dtype=stats.dtype, device=stats.device)
+    dist.all_gather_into_tensor(out, stats.contiguous(), group=group)
+    return out
+
+
+def summarize(gathered: torch.Tensor) -> dict:
+    """Totals over every env of every rank."""
+    t = gathered.to(torch.int64).sum(0).cpu().tolist()
+    return {"reward_code_sum": t[0], "done": t[1], "solved": t[2], "autoresets": t[3]}
+
+
+def max_over_ranks(seconds: float, device=None) -> float:
+    """The slowest rank's time (the job's time)."""
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return seconds
+    t = torch.tensor([seconds], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
