@@ -47,6 +47,7 @@ struct Table {
     const uint4* __restrict__ info;     // [P]
     const uint4* __restrict__ root;     // [P] trie record of each puzzle's root (sentinel if none)
     const uint4* __restrict__ trie;     // [nodes]
+    const uint64_t* __restrict__ init;  // [P] padded W = 1 layout: blocked board at reset
     uint32_t num_puzzles;
 };
 
@@ -70,15 +71,19 @@ struct Params {
     int32_t* __restrict__ err;
 };
 
-// Static puzzle rows, from global memory or from an LDS copy (same layout).
+// Static puzzle rows, from global memory or from an LDS copy (same layout).  info.w holds the
+// trie node count (low 16 bits) and the legal mask of the freshly reset puzzle (bits 16-19);
+// init[q] is the blocked board at reset (~open | start) of the padded W = 1 layout.
 template <int W>
 struct PuzzleSrc {
     const uint4* info;
     const uint4* root;
     const uint64_t* open;
+    const uint64_t* init;
     __device__ __forceinline__ uint4 get_info(uint32_t q) const { return info[q]; }
     __device__ __forceinline__ uint4 get_root(uint32_t q) const { return root[q]; }
     __device__ __forceinline__ uint64_t get_open(uint32_t q, int k) const { return open[(size_t)q * W + k]; }
+    __device__ __forceinline__ uint64_t get_init(uint32_t q) const { return init[q]; }
 };
 
 __device__ __forceinline__ int dir_dx(uint32_t d) { return d == 0 ? 1 : (d == 2 ? -1 : 0); }
@@ -119,7 +124,9 @@ __device__ __forceinline__ uint32_t uint_rand_action(uint64_t seed, uint64_t env
     return (uint32_t)(z >> 62);
 }
 
-template <int W, bool TB>
+struct RegStack;
+
+template <int W, bool TB, class Stack = RegStack>
 struct Env {
     static constexpr int D = TB ? 2 * W : 1;   // direction-stack words (32 moves per word)
     uint64_t vis[W];
@@ -140,7 +147,7 @@ struct Env {
         ty = (inf.y >> 8) & 0xFFu;
         pflags = inf.y >> 16;
         trie_base = inf.z;
-        trie_cnt = inf.w;
+        trie_cnt = inf.w & 0xFFFFu;
 #pragma unroll
         for (int k = 0; k < W; ++k) open[k] = src.get_open(q, k);
     }
@@ -194,6 +201,10 @@ struct Env {
     }
 
     // _load_puzzle (SPaRC_Gym.py:166-187) with fresh planes; no global load on this path
+    template <class Src>
+    __device__ __forceinline__ void reset(const Params& p, const Src& src, uint32_t q) {
+        reset(src, p.pitch, q);
+    }
     template <class Src>
     __device__ __forceinline__ void reset(const Src& src, uint32_t pitch, uint32_t q) {
         uint32_t sx, sy;
@@ -339,21 +350,74 @@ struct Env {
 };
 
 // ---------------------------------------------------------------------------------------------
+// Direction stacks of the W = 1 path (2 bits of information per move, <= 62 moves on a 64-bit
+// board).  In HBM both are stored as two u64 words [2][N] (move k at bits 2(k%32) of word k/32).
+struct RegStack {            // k_step / k_reset: two u64 registers
+    uint64_t lo = 0, hi = 0;
+    __device__ __forceinline__ void clear() { lo = hi = 0; }
+    __device__ __forceinline__ uint32_t read(uint32_t k) const {
+        return (uint32_t)((k < 32 ? lo : hi) >> ((k & 31u) * 2u)) & 3u;
+    }
+    __device__ __forceinline__ void write_if(bool en, uint32_t k, uint32_t d) {
+        const uint32_t sh = (k & 31u) * 2u;
+        const bool hiw = k >= 32;
+        const uint64_t w = hiw ? hi : lo;
+        const uint64_t upd = (w & ~(3ull << sh)) | ((uint64_t)d << sh);
+        lo = (en & !hiw) ? upd : lo;
+        hi = (en & hiw) ? upd : hi;
+    }
+    __device__ __forceinline__ void load(const uint64_t* d, size_t n, uint32_t i, uint32_t) {
+        lo = d[i];
+        hi = d[n + i];
+    }
+    __device__ __forceinline__ void store(uint64_t* d, size_t n, uint32_t i, uint32_t) const {
+        d[i] = lo;
+        d[n + i] = hi;
+    }
+};
+
+struct LdsStack {            // k_rollout: one byte per move in this lane's column of a per-wave
+    uint8_t* col;            // [64 moves][64 lanes] LDS array; slot 63 is a write sink
+    __device__ __forceinline__ void clear() {}
+    __device__ __forceinline__ uint32_t read(uint32_t k) const { return col[k * 64u]; }
+    __device__ __forceinline__ void write_if(bool en, uint32_t k, uint32_t d) {
+        col[(en ? k : 63u) * 64u] = (uint8_t)d;
+    }
+    __device__ __forceinline__ void load(const uint64_t* d, size_t n, uint32_t i, uint32_t moves) {
+        const uint64_t lo = d[i], hi = d[n + i];
+        for (uint32_t k = 0; k < moves; ++k)
+            col[k * 64u] = (uint8_t)(((k < 32 ? lo : hi) >> ((k & 31u) * 2u)) & 3u);
+    }
+    __device__ __forceinline__ void store(uint64_t* d, size_t n, uint32_t i, uint32_t moves) const {
+        uint64_t lo = 0, hi = 0;
+        for (uint32_t k = 0; k < moves; ++k) {
+            const uint64_t v = (uint64_t)col[k * 64u] << ((k & 31u) * 2u);
+            lo |= k < 32 ? v : 0ull;
+            hi |= k < 32 ? 0ull : v;
+        }
+        d[i] = lo;
+        d[n + i] = hi;
+    }
+};
+
+// ---------------------------------------------------------------------------------------------
 // W = 1 specialisation: lattices that fit a 64-bit board PADDED by one blocked column
 // (pitch > y_size) and one blocked row (x_size + 1 rows), i.e. (x_size + 1) * pitch <= 64
 // (every 7x7 and 5x5 pool; the host packer picks this geometry).  The agent is the bit index
 // b = x*pitch + y; `blk` = visited | not-open is the only bitboard in registers, and the four
 // neighbour tests of _get_legal_actions are one 32-bit window of blk starting at b - pitch
 // (bits 0: left, pitch-1: up, pitch+1: down, 2*pitch: right), with no bounds compares
-// (out-of-lattice neighbours are padding = blocked; below bit 0 reads as blocked).  The step is branch-free except for the
-// autoreset and the trie-record load.
-template <bool TB>
-struct Env<1, TB> {
+// (out-of-lattice neighbours are padding = blocked; below bit 0 reads as blocked).  The step is
+// branch-free except for the autoreset and the trie-record load, and is ordered so that the
+// record gathered at one step's transition is first read at the next step's transition.
+template <bool TB, class Stack>
+struct Env<1, TB, Stack> {
     uint64_t blk;        // blocked: visited | ~open (padding and gaps included)
-    uint64_t dlo, dhi;   // direction stack, 2 bits per move (<= 63 moves on a 64-bit board)
+    Stack stk;           // moves of self.path (traceback only)
     uint32_t b, len, off, node, node_term, outcome, pending, step, pid, legal, last;
     uint32_t tgt, pflags, trie_base, trie_cnt;
-    uint32_t bad = 0;    // sticky: a trie index was out of range (reported at store)
+    uint32_t prev_next = 0;   // traceback: move before the last one, read one step ahead
+    uint32_t bad = 0;         // sticky: a trie index was out of range (reported at store)
     uint4 rec;
 
     // all arms are computed unconditionally and merged with masks: a C++ ?: whose arms are
@@ -380,79 +444,88 @@ struct Env<1, TB> {
     }
 
     template <class Src>
-    __device__ __forceinline__ void load_puzzle(const Src& src, uint32_t q, uint32_t P, uint32_t& sb) {
+    __device__ __forceinline__ uint32_t load_puzzle(const Src& src, uint32_t q, uint32_t P) {
         const uint4 inf = src.get_info(q);
-        sb = ((inf.x >> 16) & 0xFFu) * P + (inf.x >> 24);
         tgt = (inf.y & 0xFFu) * P + ((inf.y >> 8) & 0xFFu);
         pflags = inf.y >> 16;
         trie_base = inf.z;
-        trie_cnt = inf.w;
+        trie_cnt = inf.w & 0xFFFFu;
+        legal = (inf.w >> 16) & 0xFu;
+        return ((inf.x >> 16) & 0xFFu) * P + (inf.x >> 24);   // start bit
     }
 
-    // node < trie_cnt always holds (host-validated tables); a violation is recorded in `bad`
-    // (reported through the error word at the end of the launch) instead of reading out of bounds
+    // The current node's record, loaded unconditionally (L2-resident table): one destination
+    // write per step keeps the compiler from merging / copying an in-flight load, so its first
+    // wait sits at the next step's trie phase.  node < trie_cnt holds on validated tables; a
+    // violation is recorded in `bad` instead of reading out of bounds.
     __device__ __forceinline__ void load_rec(const Params& p) {
         const bool oob = node >= trie_cnt;
-        bad |= oob ? 1u : 0u;
+        bad |= (oob & (bool)(pflags & 2u)) ? 1u : 0u;
         rec = p.tab.trie[trie_base + (oob ? 0u : node)];
     }
 
+    // _load_puzzle (SPaRC_Gym.py:166-187) with fresh planes: precomputed board and legal mask;
+    // the root record arrives through the next load_rec (node = 0)
     template <class Src>
-    __device__ __forceinline__ void reset(const Src& src, uint32_t P, uint32_t q) {
-        uint32_t sb;
+    __device__ __forceinline__ void reset_rows(const Src& src, uint32_t P, uint32_t q) {
         pid = q;
-        load_puzzle(src, q, P, sb);
-        b = sb;
-        blk = ~src.get_open(q, 0) | (1ull << sb);
+        b = load_puzzle(src, q, P);
+        blk = src.get_init(q);
         len = 1;
         node = 0;
         off = (pflags & 2u) ? 0u : 1u;
-        rec = src.get_root(q);
-        node_term = rec_term(rec);
+        node_term = (pflags >> 3) & 1u;   // the root is itself a solution ([start])
         outcome = 0;
         pending = 0;
         step = 0;
         last = 0;
-        dlo = dhi = 0;
-        legal = legal_mask(P);
+        stk.clear();
+    }
+    template <class Src>
+    __device__ __forceinline__ void reset(const Params& p, const Src& src, uint32_t q) {
+        reset_rows(src, p.pitch, q);
+        load_rec(p);
     }
 
     template <class Src>
     __device__ __forceinline__ int advance(const Params& p, const Src& src, uint32_t a, uint32_t& flags) {
         const uint32_t P = p.pitch;
-        if (p.autoreset == 1 && pending) {
-            const uint32_t q = pid + 1 == p.tab.num_puzzles ? 0u : pid + 1;
-            reset(src, P, q);
-            flags = (legal << 2) | 64u;
-            return 0;
-        }
-        step += (uint32_t)(step < 0x7FFFFFFFu);                                     // 1132
+        // gymnasium next-step autoreset (reset(), SPaRC_Gym.py:1087): the reset lanes run the
+        // same phases below as a no-move step whose outputs are overridden
+        const bool rst = (p.autoreset == 1) & (pending != 0);
+        if (rst) reset_rows(src, P, pid + 1 == p.tab.num_puzzles ? 0u : pid + 1);
+        // ---- phase 1: move, visited, path, legality, flags (no trie record needed)
+        step += (uint32_t)(!rst & (step < 0x7FFFFFFFu));                          // 1132
         const bool trunc0 = (int32_t)step >= p.max_steps;                          // 1134
         const uint32_t ad = a & 3u;
-        const bool moved = (a < 4u) & (bool)((legal >> ad) & 1u);                  // 1137
+        // `action in legal` (1137): bit a of the legal mask; actions >= 4 read bit 4 (always 0)
+        const uint32_t lg = rst ? 0u : legal;
+        const bool moved = (lg >> (a < 4u ? a : 4u)) & 1u;
         // neighbour offset: right +P, up -1, left -P, down +1
         const uint32_t mag = P - ((P - 1u) & (0u - (ad & 1u)));
         const uint32_t neg = 0u - ((ad ^ (ad >> 1)) & 1u);
         const uint32_t nb = b + ((mag ^ neg) - neg);
-        const bool pop = TB & moved & ((ad ^ 2u) == last) & (len >= 2);           // 1141-1166
+        // the only legal move onto a blocked (visited) cell is the traceback pop (1141-1166)
+        const bool pop = TB & moved & (bool)((blk >> (nb & 63u)) & 1ull);
         const bool fwd = moved & !pop;                                             // 1167-1188
         // visited: forward sets the new node, a pop clears the node it leaves
         const uint32_t tog = pick(fwd, nb, b);
         blk ^= (uint64_t)moved << (tog & 63u);   // (an illegal move's nb may be out of range)
         if constexpr (TB) {
-            // push `a` at move index len-1, or re-read the move before the popped one
-            const uint32_t k = pick(fwd, len - 1u, len >= 3 ? len - 3u : 0u);
-            const uint32_t sh = (k & 31u) * 2u;
-            const bool hiw = k >= 32;
-            const uint64_t wsel = hiw ? dhi : dlo;
-            const uint32_t prev = (uint32_t)(wsel >> sh) & 3u;
-            const uint64_t upd = (wsel & ~(3ull << sh)) | ((uint64_t)ad << sh);
-            dlo = (fwd & !hiw) ? upd : dlo;
-            dhi = (fwd & hiw) ? upd : dhi;
-            last = pick(fwd, ad, pick(pop, prev, last));
+            stk.write_if(fwd, len - 1u, ad);    // push `a` at move index len-1
+            last = pick(fwd, ad, pick(pop, prev_next, last));
         }
         len = len + (uint32_t)fwd - (uint32_t)pop;
-        // solution trie
+        b = pick(moved, nb, b);
+        legal = legal_mask(P);
+        const bool term = (b == tgt) & !rst;                                       // 1192
+        const bool trunc = (trunc0 | (legal == 0)) & !term & !rst;                 // 1195-1199
+        const bool done = term | trunc;
+        flags = rst ? ((legal << 2) | 64u) : ((uint32_t)term | ((uint32_t)trunc << 1) | (legal << 2));
+        pending = (uint32_t)done;
+        if constexpr (TB) prev_next = stk.read(len >= 3 ? len - 3u : 0u);   // for the next step's pop
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- phase 2: solution trie (first read of the record loaded at the previous step)
         const bool on = off == 0;
         const uint32_t c = rec_child(rec, ad);
         const bool down = fwd & on & (c != kNone);
@@ -460,22 +533,15 @@ struct Env<1, TB> {
         node_term = pick(down, rec_child_term(rec, ad), pick(up, rec_parent_term(rec), node_term));
         node = pick(down, c, pick(up, rec_parent(rec), node));
         off = pick(on, (uint32_t)(fwd & (c == kNone)), off + (uint32_t)fwd - (uint32_t)pop);
-        if (down | up) load_rec(p);
-        b = pick(moved, nb, b);
-        legal = legal_mask(P);
-        const bool term = b == tgt;                                                // 1192
-        const bool trunc = (trunc0 | (legal == 0)) & !term;                        // 1195-1199
-        const bool done = term | trunc;
+        load_rec(p);
+        // ---- phase 3: reward code (1204-1223): done: +100 on a solution, else -100 unless the
+        // previous done step already set outcome_reward = 1 (then 0); otherwise +-1 when moved
+        // (0 if the puzzle has no solutions); an autoreset step returns 0
         const bool match = (off == 0) & (node_term != 0);
-        // reward code (1204-1223): done: +100 on a solution, else -100 unless the previous done
-        // step already set outcome_reward = 1 (then 0); otherwise +-1 when moved (0 if no solutions)
         const int c_done = match ? 100 : (outcome != 1 ? -100 : 0);
         const int c_move = (moved & (bool)(pflags & 1u)) ? (off == 0 ? 1 : -1) : 0;
-        const int code = done ? c_done : c_move;
         outcome = pick(done, pick(match | (outcome == 1), 1u, 2u), 0u);
-        pending = (uint32_t)done;
-        flags = (uint32_t)term | ((uint32_t)trunc << 1) | (legal << 2);
-        return code;
+        return done ? c_done : c_move;
     }
 
     template <class Src>
@@ -483,12 +549,6 @@ struct Env<1, TB> {
         const State& s = p.st;
         const uint32_t P = p.pitch;
         const uint64_t vis = s.vis[i];
-        if constexpr (TB) {
-            dlo = s.dirs[i];
-            dhi = s.dirs[(size_t)p.n + i];
-        } else {
-            dlo = dhi = 0;
-        }
         const uint32_t ps = s.pos[i], ax = s.aux[i];
         b = (ps & 0xFFu) * P + ((ps >> 8) & 0xFFu);
         len = (ps >> 16) & 0xFFu;
@@ -500,14 +560,13 @@ struct Env<1, TB> {
         step = s.step[i];
         pid = s.pid[i];
         bad = 0;
-        uint32_t sb;
-        load_puzzle(src, pid, P, sb);
-        blk = vis | ~src.get_open(pid, 0);
-        if (pflags & 2u) load_rec(p);
-        else rec = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, kNone, 0u);
+        load_puzzle(src, pid, P);
+        blk = vis | ~p.tab.open[pid];
+        load_rec(p);
         if constexpr (TB) {
-            const uint32_t k = len >= 2 ? len - 2 : 0u;
-            last = (uint32_t)((k < 32 ? dlo : dhi) >> ((k & 31u) * 2u)) & 3u;
+            stk.load(s.dirs, p.n, i, len >= 1 ? len - 1 : 0u);
+            last = len >= 2 ? stk.read(len - 2) : 0u;
+            prev_next = stk.read(len >= 3 ? len - 3u : 0u);
         } else {
             last = 0;
         }
@@ -518,11 +577,10 @@ struct Env<1, TB> {
     __device__ __forceinline__ void store(const Params& p, const Src& src, uint32_t i) const {
         const State& s = p.st;
         const uint32_t P = p.pitch;
-        s.vis[i] = blk & src.get_open(pid, 0);
-        if constexpr (TB) {
-            s.dirs[i] = dlo;
-            s.dirs[(size_t)p.n + i] = dhi;
-        }
+        const uint4 inf = src.get_info(pid);
+        const uint32_t sb = ((inf.x >> 16) & 0xFFu) * P + (inf.x >> 24);
+        s.vis[i] = blk & (p.tab.open[pid] | (1ull << sb));     // the start is always visited
+        if constexpr (TB) stk.store(s.dirs, p.n, i, len >= 1 ? len - 1 : 0u);
         const uint32_t x = b / P, y = b - x * P;
         s.pos[i] = x | (y << 8) | (len << 16) | (off << 24);
         s.aux[i] = node | (outcome << 16) | (pending << 18) | (node_term << 19);

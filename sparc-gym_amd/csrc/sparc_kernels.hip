@@ -28,11 +28,19 @@ constexpr int kBlock = 256;
 constexpr int kTile = 16;                             // env-steps per LDS-transposed I/O tile
 constexpr int kTileBytes = 3 * 64 * kTile;            // per wave: actions, reward codes, flags
 constexpr int kTilesLds = (kBlock / 64) * kTileBytes;  // 12 KiB per workgroup
-constexpr size_t kMaxDynLds = 64 * 1024;
+constexpr size_t kMaxDynLds = 128 * 1024;
 
+// LDS bytes of the staged puzzle rows: info + root record + (W = 1) the reset board, or
+// (W > 1) the open bitboard that the generic step reads every step
 template <int W>
 __host__ __device__ constexpr size_t table_lds_bytes(uint32_t P) {
     return (size_t)P * (2 * sizeof(uint4) + W * sizeof(uint64_t));
+}
+// per-wave LDS direction stack of the W = 1 traceback rollout: [64 moves][64 lanes] bytes
+constexpr size_t kStackBytes = 64 * 64;
+template <int W, bool TB>
+__host__ __device__ constexpr size_t stack_lds_bytes() {
+    return (W == 1 && TB) ? (kBlock / 64) * kStackBytes : 0;
 }
 
 template <int W, bool TB>
@@ -46,9 +54,9 @@ __global__ void __launch_bounds__(kBlock) k_reset(Params p, const uint32_t* __re
         atomicOr(p.err, (int)kErrPuzzle);
         return;
     }
-    const PuzzleSrc<W> src{p.tab.info, p.tab.root, p.tab.open};
+    const PuzzleSrc<W> src{p.tab.info, p.tab.root, p.tab.open, p.tab.init};
     Env<W, TB> e;
-    e.reset(src, p.pitch, pid);
+    e.reset(p, src, pid);
     e.store(p, src, i);
     if (flg) flg[i] = (uint8_t)(e.legal << 2);
 }
@@ -58,7 +66,7 @@ __global__ void __launch_bounds__(kBlock) k_step(Params p, const uint8_t* __rest
                                                  int8_t* __restrict__ rew, uint8_t* __restrict__ flg) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= p.n) return;
-    const PuzzleSrc<W> src{p.tab.info, p.tab.root, p.tab.open};
+    const PuzzleSrc<W> src{p.tab.info, p.tab.root, p.tab.open, p.tab.init};
     Env<W, TB> e;
     e.load(p, src, i);
     uint32_t f;
@@ -97,24 +105,28 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
                                                     uint64_t seed, uint64_t t0, int8_t* __restrict__ rew,
                                                     uint8_t* __restrict__ flg, int4* __restrict__ stats,
                                                     uint32_t tiled) {
+    // LDS: [I/O tiles, 3 KiB per wave][W=1 traceback: move stacks, 4 KiB per wave][puzzle rows]
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint8_t* ta = smem + wv * kTileBytes;
     uint8_t* tr = ta + 64 * kTile;
     uint8_t* tf = tr + 64 * kTile;
-    PuzzleSrc<W> src{p.tab.info, p.tab.root, p.tab.open};
+    constexpr size_t kStackOff = kTilesLds, kTableOff = kTilesLds + stack_lds_bytes<W, TB>();
+    PuzzleSrc<W> src{p.tab.info, p.tab.root, p.tab.open, p.tab.init};
     if constexpr (LDS_TABLE) {
         const uint32_t P = p.tab.num_puzzles;
-        uint4* linfo = reinterpret_cast<uint4*>(smem + kTilesLds);
+        uint4* linfo = reinterpret_cast<uint4*>(smem + kTableOff);
         uint4* lroot = linfo + P;
-        uint64_t* lopen = reinterpret_cast<uint64_t*>(lroot + P);
+        uint64_t* lrow = reinterpret_cast<uint64_t*>(lroot + P);   // W=1: init board, else open
+        const uint64_t* grow = W == 1 ? p.tab.init : p.tab.open;
         for (uint32_t k = threadIdx.x; k < P; k += kBlock) {
             linfo[k] = p.tab.info[k];
             lroot[k] = p.tab.root[k];
         }
-        for (uint32_t k = threadIdx.x; k < P * W; k += kBlock) lopen[k] = p.tab.open[k];
+        for (uint32_t k = threadIdx.x; k < P * W; k += kBlock) lrow[k] = grow[k];
         __syncthreads();
-        src = PuzzleSrc<W>{linfo, lroot, lopen};
+        if constexpr (W == 1) src = PuzzleSrc<W>{linfo, lroot, p.tab.open, lrow};
+        else src = PuzzleSrc<W>{linfo, lroot, lrow, p.tab.init};
     }
     const uint32_t wave_base = blockIdx.x * kBlock + wv * 64;
     if (wave_base >= p.n) return;
@@ -124,7 +136,9 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
     const size_t n = p.n;
     const uint64_t gid = p.env_offset + i;
     const uint32_t r = lane >> 2, c = (lane & 3) * 16;   // this lane's 16-byte piece of a tile
-    Env<W, TB> e;
+    using Stack = typename std::conditional<(W == 1 && TB), LdsStack, RegStack>::type;
+    Env<W, TB, Stack> e;
+    if constexpr (W == 1 && TB) e.stk.col = smem + kStackOff + wv * kStackBytes + lane;
     if (active) e.load(p, src, i);
     int4 acc = make_int4(0, 0, 0, 0);
     u32x4 anext = {0u, 0u, 0u, 0u};
@@ -139,17 +153,26 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
                 *reinterpret_cast<u32x4*>(ta + r * 64 + c) = acur;
                 wave_lds_fence();
             }
-#pragma unroll 4
-            for (int k = 0; k < kTile; ++k) {
-                const uint32_t a = RAND ? uint_rand_action(seed, gid, t0 + (uint64_t)(tb + k)) : ta[k * 64 + lane];
-                uint32_t f;
-                const int code = e.advance(p, src, a, f);
-                tr[k * 64 + lane] = (uint8_t)code;
-                tf[k * 64 + lane] = (uint8_t)f;
-                acc.x += code;
-                acc.y += (f & 3u) ? 1 : 0;
-                acc.z += ((f & 3u) && code == 100) ? 1 : 0;
-                acc.w += (f & 64u) ? 1 : 0;
+            // 4 groups of 4 steps: each group reads its 4 actions first (one LDS wait), then
+            // steps; a full 16-step unroll spills SGPRs
+#pragma unroll 1
+            for (int g = 0; g < kTile; g += 4) {
+                uint32_t av[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    av[j] = RAND ? uint_rand_action(seed, gid, t0 + (uint64_t)(tb + g + j)) : ta[(g + j) * 64 + lane];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int k = g + j;
+                    uint32_t f;
+                    const int code = e.advance(p, src, av[j], f);
+                    tr[k * 64 + lane] = (uint8_t)code;
+                    tf[k * 64 + lane] = (uint8_t)f;
+                    acc.x += code;
+                    acc.y += (f & 3u) ? 1 : 0;
+                    acc.z += ((f & 3u) && code == 100) ? 1 : 0;
+                    acc.w += (f & 64u) ? 1 : 0;
+                }
             }
             wave_lds_fence();
             const size_t o = (size_t)(tb + r) * n + wave_base + c;
@@ -216,6 +239,7 @@ struct Ctx {
     uint32_t *pos = nullptr, *aux = nullptr, *step = nullptr, *pid = nullptr;
     uint64_t* t_open = nullptr;
     uint4 *t_info = nullptr, *t_root = nullptr, *t_trie = nullptr;
+    uint64_t* t_init = nullptr;
     int32_t* err = nullptr;
     uint8_t *s_act = nullptr, *s_flags = nullptr, *s_mask = nullptr;
     int8_t* s_rew = nullptr;
@@ -244,6 +268,7 @@ Params make_params(const Ctx* c) {
     p.tab.info = c->t_info;
     p.tab.root = c->t_root;
     p.tab.trie = c->t_trie;
+    p.tab.init = c->t_init;
     p.tab.num_puzzles = c->num_puzzles;
     p.st.vis = c->vis;
     p.st.dirs = c->dirs;
@@ -346,7 +371,7 @@ int sparc_destroy(void* ctx) {
     if (!c) return SPARC_OK;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void* bufs[] = {c->vis, c->dirs, c->pos, c->aux, c->step, c->pid, c->t_open, c->t_info, c->t_root, c->t_trie,
+    void* bufs[] = {c->vis, c->dirs, c->pos, c->aux, c->step, c->pid, c->t_open, c->t_info, c->t_root, c->t_trie, c->t_init,
                     c->err, c->s_act, c->s_flags, c->s_mask, c->s_rew, c->s_pidx};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -431,6 +456,8 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
     if (c->t_info) HIPCHK(c, hipFree(c->t_info));
     if (c->t_trie) HIPCHK(c, hipFree(c->t_trie));
     if (c->t_root) HIPCHK(c, hipFree(c->t_root));
+    if (c->t_init) HIPCHK(c, hipFree(c->t_init));
+    c->t_init = nullptr;
     c->t_open = nullptr;
     c->t_info = nullptr;
     c->t_root = nullptr;
@@ -451,7 +478,32 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
     }
     HIPCHK(c, hipMemcpy(c->t_root, roots.data(), sizeof(uint4) * P, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->t_open, t->open, sizeof(uint64_t) * P * W, hipMemcpyHostToDevice));
-    HIPCHK(c, hipMemcpy(c->t_info, t->info, sizeof(uint4) * P, hipMemcpyHostToDevice));
+    // device copy of info: w3 = trie node count | legal mask of the reset state << 16, and the
+    // reset board (~open | start) of the padded W = 1 layout
+    std::vector<uint4> dinfo(P);
+    std::vector<uint64_t> init(P, 0);
+    for (size_t q = 0; q < P; ++q) {
+        const uint32_t* inf = t->info + 4 * q;
+        const uint32_t X = inf[0] & 0xFF, Y = (inf[0] >> 8) & 0xFF;
+        const uint32_t sx = (inf[0] >> 16) & 0xFF, sy = inf[0] >> 24;
+        auto open_at = [&](uint32_t x, uint32_t y) {
+            const uint32_t b = x * pitch + y;
+            return (t->open[q * W + (b >> 6)] >> (b & 63)) & 1ull;
+        };
+        uint32_t legal0 = 0;
+        const int dx[4] = {1, 0, -1, 0}, dy[4] = {0, -1, 0, 1};
+        for (int d = 0; d < 4; ++d) {
+            const int nx = (int)sx + dx[d], ny = (int)sy + dy[d];
+            if (nx >= 0 && ny >= 0 && nx < (int)X && ny < (int)Y && open_at(nx, ny)) legal0 |= 1u << d;
+        }
+        const uint32_t root_term = ((inf[1] >> 16) & 2u) ? ((roots[q].z >> 16) & 1u) : 0u;
+        dinfo[q] = make_uint4(inf[0], (inf[1] & 0x0007FFFFu) | (root_term << 19), inf[2],
+                              (inf[3] & 0xFFFFu) | (legal0 << 16));
+        if (W == 1) init[q] = ~t->open[q] | (1ull << (sx * pitch + sy));
+    }
+    HIPCHK(c, hipMalloc(&c->t_init, sizeof(uint64_t) * P));
+    HIPCHK(c, hipMemcpy(c->t_info, dinfo.data(), sizeof(uint4) * P, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->t_init, init.data(), sizeof(uint64_t) * P, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemset(c->t_trie, 0xFF, sizeof(uint4) * nn));
     if (t->num_nodes > 0)
         HIPCHK(c, hipMemcpy(c->t_trie, t->trie, sizeof(uint4) * (size_t)t->num_nodes, hipMemcpyHostToDevice));
@@ -539,20 +591,23 @@ int sparc_rollout_device(void* ctx, int32_t T, const uint8_t* d_act, uint64_t se
     dispatch_w_tb(c->W, c->cfg.traceback, [&](auto w, auto tb) {
         constexpr int W = decltype(w)::value;
         constexpr bool TB = decltype(tb)::value;
+        const size_t base = kTilesLds + stack_lds_bytes<W, TB>();
         const size_t tbytes = table_lds_bytes<W>(c->num_puzzles);
-        const bool lds_table = kTilesLds + tbytes <= budget;
-        const size_t shm = kTilesLds + (lds_table ? tbytes : 0);
+        const bool lds_table = base + tbytes <= budget;
+        const size_t shm = base + (lds_table ? tbytes : 0);
         const dim3 g = grid_for(c->n);
+        auto launch = [&](auto kern, const uint8_t* a) {
+            if (shm > 64 * 1024)
+                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+            kern<<<g, kBlock, shm, c->stream>>>(p, T, a, seed, t0, d_rew, d_flags, st, tiled);
+        };
         if (d_act) {
-            if (lds_table)
-                k_rollout<W, TB, false, true><<<g, kBlock, shm, c->stream>>>(p, T, d_act, seed, t0, d_rew, d_flags, st, tiled);
-            else
-                k_rollout<W, TB, false, false><<<g, kBlock, shm, c->stream>>>(p, T, d_act, seed, t0, d_rew, d_flags, st, tiled);
+            if (lds_table) launch(k_rollout<W, TB, false, true>, d_act);
+            else launch(k_rollout<W, TB, false, false>, d_act);
         } else {
-            if (lds_table)
-                k_rollout<W, TB, true, true><<<g, kBlock, shm, c->stream>>>(p, T, nullptr, seed, t0, d_rew, d_flags, st, tiled);
-            else
-                k_rollout<W, TB, true, false><<<g, kBlock, shm, c->stream>>>(p, T, nullptr, seed, t0, d_rew, d_flags, st, tiled);
+            if (lds_table) launch(k_rollout<W, TB, true, true>, nullptr);
+            else launch(k_rollout<W, TB, true, false>, nullptr);
         }
     });
     return launch_check(c);
