@@ -48,6 +48,7 @@ struct Table {
     const uint4* __restrict__ root;     // [P] trie record of each puzzle's root (sentinel if none)
     const uint4* __restrict__ trie;     // [nodes]
     const uint64_t* __restrict__ init;  // [P] padded W = 1 layout: blocked board at reset
+    const uint4* __restrict__ row1;     // [P] padded W = 1 layout: compact puzzle row
     uint32_t num_puzzles;
 };
 
@@ -80,6 +81,9 @@ struct PuzzleSrc {
     const uint4* root;
     const uint64_t* open;
     const uint64_t* init;
+    const uint4* row1;     // W = 1: {start_bit | target_bit<<8 | flags<<16, trie_base,
+                           //         trie_cnt | legal0<<16, 0}
+    __device__ __forceinline__ uint4 get_row1(uint32_t q) const { return row1[q]; }
     __device__ __forceinline__ uint4 get_info(uint32_t q) const { return info[q]; }
     __device__ __forceinline__ uint4 get_root(uint32_t q) const { return root[q]; }
     __device__ __forceinline__ uint64_t get_open(uint32_t q, int k) const { return open[(size_t)q * W + k]; }
@@ -433,8 +437,8 @@ struct Env<1, TB, Stack> {
         const uint32_t above = (uint32_t)(blk >> sr);
         const uint32_t below = (uint32_t)(blk << sl) | ((1u << sl) - 1u);
         const uint32_t w = ~pick(b >= P, above, below);                 // free bits (2P + 1 <= 31)
-        uint32_t m = ((w >> (2 * P)) & 1u) | (((w >> (P - 1)) & 1u) << 1) | ((w & 1u) << 2) |
-                     (((w >> (P + 1)) & 1u) << 3);
+        // up (bit P-1) and down (bit P+1) land on bits 1 and 3 with one shift and mask
+        uint32_t m = (((w >> (P - 1)) & 5u) << 1) | ((w >> (2 * P)) & 1u) | ((w << 2) & 4u);
         if constexpr (TB) {
             // path[-2] is the reverse of the last move; it is open unless it is a closed start
             const uint32_t back = (uint32_t)(len >= 3) | ((uint32_t)(len == 2) & ((~pflags >> 2) & 1u));
@@ -444,14 +448,14 @@ struct Env<1, TB, Stack> {
     }
 
     template <class Src>
-    __device__ __forceinline__ uint32_t load_puzzle(const Src& src, uint32_t q, uint32_t P) {
-        const uint4 inf = src.get_info(q);
-        tgt = (inf.y & 0xFFu) * P + ((inf.y >> 8) & 0xFFu);
-        pflags = inf.y >> 16;
-        trie_base = inf.z;
-        trie_cnt = inf.w & 0xFFFFu;
-        legal = (inf.w >> 16) & 0xFu;
-        return ((inf.x >> 16) & 0xFFu) * P + (inf.x >> 24);   // start bit
+    __device__ __forceinline__ uint32_t load_puzzle(const Src& src, uint32_t q, uint32_t) {
+        const uint4 r = src.get_row1(q);
+        tgt = (r.x >> 8) & 0xFFu;
+        pflags = r.x >> 16;
+        trie_base = r.y;
+        trie_cnt = r.z & 0xFFFFu;
+        legal = r.z >> 16;
+        return r.x & 0xFFu;   // start bit
     }
 
     // The current node's record, loaded unconditionally (L2-resident table): one destination
@@ -521,13 +525,13 @@ struct Env<1, TB, Stack> {
         const bool term = (b == tgt) & !rst;                                       // 1192
         const bool trunc = (trunc0 | (legal == 0)) & !term & !rst;                 // 1195-1199
         const bool done = term | trunc;
-        flags = rst ? ((legal << 2) | 64u) : ((uint32_t)term | ((uint32_t)trunc << 1) | (legal << 2));
+        flags = (legal << 2) | pick(rst, 64u, (uint32_t)term | ((uint32_t)trunc << 1));
         pending = (uint32_t)done;
         if constexpr (TB) prev_next = stk.read(len >= 3 ? len - 3u : 0u);   // for the next step's pop
         __builtin_amdgcn_sched_barrier(0);
         // ---- phase 2: solution trie (first read of the record loaded at the previous step)
         const bool on = off == 0;
-        const uint32_t c = rec_child(rec, ad);
+        const uint32_t c = (uint32_t)((((uint64_t)rec.y << 32) | rec.x) >> (ad * 16u)) & 0xFFFFu;
         const bool down = fwd & on & (c != kNone);
         const bool up = pop & on;
         node_term = pick(down, rec_child_term(rec, ad), pick(up, rec_parent_term(rec), node_term));
@@ -577,8 +581,7 @@ struct Env<1, TB, Stack> {
     __device__ __forceinline__ void store(const Params& p, const Src& src, uint32_t i) const {
         const State& s = p.st;
         const uint32_t P = p.pitch;
-        const uint4 inf = src.get_info(pid);
-        const uint32_t sb = ((inf.x >> 16) & 0xFFu) * P + (inf.x >> 24);
+        const uint32_t sb = src.get_row1(pid).x & 0xFFu;
         s.vis[i] = blk & (p.tab.open[pid] | (1ull << sb));     // the start is always visited
         if constexpr (TB) stk.store(s.dirs, p.n, i, len >= 1 ? len - 1 : 0u);
         const uint32_t x = b / P, y = b - x * P;

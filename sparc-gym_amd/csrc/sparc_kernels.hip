@@ -30,11 +30,12 @@ constexpr int kTileBytes = 3 * 64 * kTile;            // per wave: actions, rewa
 constexpr int kTilesLds = (kBlock / 64) * kTileBytes;  // 12 KiB per workgroup
 constexpr size_t kMaxDynLds = 128 * 1024;
 
-// LDS bytes of the staged puzzle rows: info + root record + (W = 1) the reset board, or
-// (W > 1) the open bitboard that the generic step reads every step
+// LDS bytes of the staged puzzle rows: (W = 1) compact row + reset board, or (W > 1) info +
+// root record + the open bitboard that the generic step reads every step
 template <int W>
 __host__ __device__ constexpr size_t table_lds_bytes(uint32_t P) {
-    return (size_t)P * (2 * sizeof(uint4) + W * sizeof(uint64_t));
+    return W == 1 ? (size_t)P * (sizeof(uint4) + sizeof(uint64_t))
+                  : (size_t)P * (2 * sizeof(uint4) + W * sizeof(uint64_t));
 }
 // per-wave LDS direction stack of the W = 1 traceback rollout: [64 moves][64 lanes] bytes
 constexpr size_t kStackBytes = 64 * 64;
@@ -54,7 +55,7 @@ __global__ void __launch_bounds__(kBlock) k_reset(Params p, const uint32_t* __re
         atomicOr(p.err, (int)kErrPuzzle);
         return;
     }
-    const PuzzleSrc<W> src{p.tab.info, p.tab.root, p.tab.open, p.tab.init};
+    const PuzzleSrc<W> src{p.tab.info, p.tab.root, p.tab.open, p.tab.init, p.tab.row1};
     Env<W, TB> e;
     e.reset(p, src, pid);
     e.store(p, src, i);
@@ -66,7 +67,7 @@ __global__ void __launch_bounds__(kBlock) k_step(Params p, const uint8_t* __rest
                                                  int8_t* __restrict__ rew, uint8_t* __restrict__ flg) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= p.n) return;
-    const PuzzleSrc<W> src{p.tab.info, p.tab.root, p.tab.open, p.tab.init};
+    const PuzzleSrc<W> src{p.tab.info, p.tab.root, p.tab.open, p.tab.init, p.tab.row1};
     Env<W, TB> e;
     e.load(p, src, i);
     uint32_t f;
@@ -112,21 +113,30 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
     uint8_t* tr = ta + 64 * kTile;
     uint8_t* tf = tr + 64 * kTile;
     constexpr size_t kStackOff = kTilesLds, kTableOff = kTilesLds + stack_lds_bytes<W, TB>();
-    PuzzleSrc<W> src{p.tab.info, p.tab.root, p.tab.open, p.tab.init};
+    PuzzleSrc<W> src{p.tab.info, p.tab.root, p.tab.open, p.tab.init, p.tab.row1};
     if constexpr (LDS_TABLE) {
         const uint32_t P = p.tab.num_puzzles;
-        uint4* linfo = reinterpret_cast<uint4*>(smem + kTableOff);
-        uint4* lroot = linfo + P;
-        uint64_t* lrow = reinterpret_cast<uint64_t*>(lroot + P);   // W=1: init board, else open
-        const uint64_t* grow = W == 1 ? p.tab.init : p.tab.open;
-        for (uint32_t k = threadIdx.x; k < P; k += kBlock) {
-            linfo[k] = p.tab.info[k];
-            lroot[k] = p.tab.root[k];
+        if constexpr (W == 1) {
+            uint4* lrow1 = reinterpret_cast<uint4*>(smem + kTableOff);
+            uint64_t* linit = reinterpret_cast<uint64_t*>(lrow1 + P);
+            for (uint32_t k = threadIdx.x; k < P; k += kBlock) {
+                lrow1[k] = p.tab.row1[k];
+                linit[k] = p.tab.init[k];
+            }
+            __syncthreads();
+            src = PuzzleSrc<W>{p.tab.info, p.tab.root, p.tab.open, linit, lrow1};
+        } else {
+            uint4* linfo = reinterpret_cast<uint4*>(smem + kTableOff);
+            uint4* lroot = linfo + P;
+            uint64_t* lopen = reinterpret_cast<uint64_t*>(lroot + P);
+            for (uint32_t k = threadIdx.x; k < P; k += kBlock) {
+                linfo[k] = p.tab.info[k];
+                lroot[k] = p.tab.root[k];
+            }
+            for (uint32_t k = threadIdx.x; k < P * W; k += kBlock) lopen[k] = p.tab.open[k];
+            __syncthreads();
+            src = PuzzleSrc<W>{linfo, lroot, lopen, p.tab.init, p.tab.row1};
         }
-        for (uint32_t k = threadIdx.x; k < P * W; k += kBlock) lrow[k] = grow[k];
-        __syncthreads();
-        if constexpr (W == 1) src = PuzzleSrc<W>{linfo, lroot, p.tab.open, lrow};
-        else src = PuzzleSrc<W>{linfo, lroot, lrow, p.tab.init};
     }
     const uint32_t wave_base = blockIdx.x * kBlock + wv * 64;
     if (wave_base >= p.n) return;
@@ -240,6 +250,7 @@ struct Ctx {
     uint64_t* t_open = nullptr;
     uint4 *t_info = nullptr, *t_root = nullptr, *t_trie = nullptr;
     uint64_t* t_init = nullptr;
+    uint4* t_row1 = nullptr;
     int32_t* err = nullptr;
     uint8_t *s_act = nullptr, *s_flags = nullptr, *s_mask = nullptr;
     int8_t* s_rew = nullptr;
@@ -269,6 +280,7 @@ Params make_params(const Ctx* c) {
     p.tab.root = c->t_root;
     p.tab.trie = c->t_trie;
     p.tab.init = c->t_init;
+    p.tab.row1 = c->t_row1;
     p.tab.num_puzzles = c->num_puzzles;
     p.st.vis = c->vis;
     p.st.dirs = c->dirs;
@@ -371,7 +383,7 @@ int sparc_destroy(void* ctx) {
     if (!c) return SPARC_OK;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void* bufs[] = {c->vis, c->dirs, c->pos, c->aux, c->step, c->pid, c->t_open, c->t_info, c->t_root, c->t_trie, c->t_init,
+    void* bufs[] = {c->vis, c->dirs, c->pos, c->aux, c->step, c->pid, c->t_open, c->t_info, c->t_root, c->t_trie, c->t_init, c->t_row1,
                     c->err, c->s_act, c->s_flags, c->s_mask, c->s_rew, c->s_pidx};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -457,7 +469,9 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
     if (c->t_trie) HIPCHK(c, hipFree(c->t_trie));
     if (c->t_root) HIPCHK(c, hipFree(c->t_root));
     if (c->t_init) HIPCHK(c, hipFree(c->t_init));
+    if (c->t_row1) HIPCHK(c, hipFree(c->t_row1));
     c->t_init = nullptr;
+    c->t_row1 = nullptr;
     c->t_open = nullptr;
     c->t_info = nullptr;
     c->t_root = nullptr;
@@ -482,6 +496,7 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
     // reset board (~open | start) of the padded W = 1 layout
     std::vector<uint4> dinfo(P);
     std::vector<uint64_t> init(P, 0);
+    std::vector<uint4> row1(P, make_uint4(0u, 0u, 0u, 0u));
     for (size_t q = 0; q < P; ++q) {
         const uint32_t* inf = t->info + 4 * q;
         const uint32_t X = inf[0] & 0xFF, Y = (inf[0] >> 8) & 0xFF;
@@ -499,8 +514,15 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
         const uint32_t root_term = ((inf[1] >> 16) & 2u) ? ((roots[q].z >> 16) & 1u) : 0u;
         dinfo[q] = make_uint4(inf[0], (inf[1] & 0x0007FFFFu) | (root_term << 19), inf[2],
                               (inf[3] & 0xFFFFu) | (legal0 << 16));
-        if (W == 1) init[q] = ~t->open[q] | (1ull << (sx * pitch + sy));
+        if (W == 1) {
+            const uint32_t tx = inf[1] & 0xFF, ty = (inf[1] >> 8) & 0xFF;
+            init[q] = ~t->open[q] | (1ull << (sx * pitch + sy));
+            row1[q] = make_uint4((sx * pitch + sy) | ((tx * pitch + ty) << 8) | (dinfo[q].y & 0xFFFF0000u),
+                                 inf[2], (inf[3] & 0xFFFFu) | (legal0 << 16), 0u);
+        }
     }
+    HIPCHK(c, hipMalloc(&c->t_row1, sizeof(uint4) * P));
+    HIPCHK(c, hipMemcpy(c->t_row1, row1.data(), sizeof(uint4) * P, hipMemcpyHostToDevice));
     HIPCHK(c, hipMalloc(&c->t_init, sizeof(uint64_t) * P));
     HIPCHK(c, hipMemcpy(c->t_info, dinfo.data(), sizeof(uint4) * P, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->t_init, init.data(), sizeof(uint64_t) * P, hipMemcpyHostToDevice));
