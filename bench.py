@@ -44,7 +44,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
-    ap.add_argument("--chunk", type=int, default=500, help="env-steps per rollout launch")
+    ap.add_argument("--chunk", type=int, default=0,
+                    help="env-steps per rollout launch (0 = all timed steps in one launch)")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--mode", default="rollout", choices=["rollout", "step"])
     ap.add_argument("--puzzles", type=int, default=1024)
@@ -118,7 +120,9 @@ def main():
     from sparc_gym_amd import dist as sdist
     from sparc_gym_amd.puzzles import pack_table, process_puzzles
 
-    rank, world, local = sdist.init_from_env("nccl")
+    rank, world, local = sdist.init_from_env(args.backend)
+    local = local % max(1, torch.cuda.device_count())   # (rehearsals: several ranks on one GPU)
+    torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
     sizes, full, tb = CONFIGS[args.config]
@@ -132,7 +136,7 @@ def main():
     vec.reset(options={"puzzle_index": (gid * 2654435761 % len(proc)).astype(np.int64)})
 
     K, W = args.steps, args.warmup
-    chunk = max(1, min(args.chunk, K))
+    chunk = K if args.chunk <= 0 else max(1, min(args.chunk, K))
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
     actions = torch.randint(0, 4, (K, n), dtype=torch.uint8, device=dev, generator=g)

@@ -380,22 +380,23 @@ struct RegStack {            // k_step / k_reset: two u64 registers
     }
 };
 
-struct LdsStack {            // k_rollout: one byte per move in this lane's column of a per-wave
-    uint8_t* col;            // [64 moves][64 lanes] LDS array; slot 63 is a write sink
+template <uint32_t S>         // k_rollout: one byte per move in this lane's column of a per-wave
+struct LdsStack {            // [64 moves][S lanes] LDS array; slot 63 is a write sink
+    uint8_t* col;
     __device__ __forceinline__ void clear() {}
-    __device__ __forceinline__ uint32_t read(uint32_t k) const { return col[k * 64u]; }
+    __device__ __forceinline__ uint32_t read(uint32_t k) const { return col[k * S]; }
     __device__ __forceinline__ void write_if(bool en, uint32_t k, uint32_t d) {
-        col[(en ? k : 63u) * 64u] = (uint8_t)d;
+        col[(en ? k : 63u) * S] = (uint8_t)d;
     }
     __device__ __forceinline__ void load(const uint64_t* d, size_t n, uint32_t i, uint32_t moves) {
         const uint64_t lo = d[i], hi = d[n + i];
         for (uint32_t k = 0; k < moves; ++k)
-            col[k * 64u] = (uint8_t)(((k < 32 ? lo : hi) >> ((k & 31u) * 2u)) & 3u);
+            col[k * S] = (uint8_t)(((k < 32 ? lo : hi) >> ((k & 31u) * 2u)) & 3u);
     }
     __device__ __forceinline__ void store(uint64_t* d, size_t n, uint32_t i, uint32_t moves) const {
         uint64_t lo = 0, hi = 0;
         for (uint32_t k = 0; k < moves; ++k) {
-            const uint64_t v = (uint64_t)col[k * 64u] << ((k & 31u) * 2u);
+            const uint64_t v = (uint64_t)col[k * S] << ((k & 31u) * 2u);
             lo |= k < 32 ? v : 0ull;
             hi |= k < 32 ? 0ull : v;
         }
@@ -537,7 +538,9 @@ struct Env<1, TB, Stack> {
         node_term = pick(down, rec_child_term(rec, ad), pick(up, rec_parent_term(rec), node_term));
         node = pick(down, c, pick(up, rec_parent(rec), node));
         off = pick(on, (uint32_t)(fwd & (c == kNone)), off + (uint32_t)fwd - (uint32_t)pop);
+#ifndef SPARC_DIAG_NO_TRIE_LOAD
         load_rec(p);
+#endif
         // ---- phase 3: reward code (1204-1223): done: +100 on a solution, else -100 unless the
         // previous done step already set outcome_reward = 1 (then 0); otherwise +-1 when moved
         // (0 if the puzzle has no solutions); an autoreset step returns 0

@@ -26,8 +26,10 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kTile = 16;                             // env-steps per LDS-transposed I/O tile
-constexpr int kTileBytes = 3 * 64 * kTile;            // per wave: actions, reward codes, flags
-constexpr int kTilesLds = (kBlock / 64) * kTileBytes;  // 12 KiB per workgroup
+constexpr int kWaves = kBlock / 64;
+// per-wave LDS I/O tiles (actions, reward codes, flags), EPW envs per wave
+template <int EPW>
+__host__ __device__ constexpr size_t tiles_lds_bytes() { return (size_t)kWaves * 3 * EPW * kTile; }
 constexpr size_t kMaxDynLds = 128 * 1024;
 
 // LDS bytes of the staged puzzle rows: (W = 1) compact row + reset board, or (W > 1) info +
@@ -37,11 +39,10 @@ __host__ __device__ constexpr size_t table_lds_bytes(uint32_t P) {
     return W == 1 ? (size_t)P * (sizeof(uint4) + sizeof(uint64_t))
                   : (size_t)P * (2 * sizeof(uint4) + W * sizeof(uint64_t));
 }
-// per-wave LDS direction stack of the W = 1 traceback rollout: [64 moves][64 lanes] bytes
-constexpr size_t kStackBytes = 64 * 64;
-template <int W, bool TB>
+// per-wave LDS direction stack of the W = 1 traceback rollout: [64 moves][EPW lanes] bytes
+template <int W, bool TB, int EPW>
 __host__ __device__ constexpr size_t stack_lds_bytes() {
-    return (W == 1 && TB) ? (kBlock / 64) * kStackBytes : 0;
+    return (W == 1 && TB) ? (size_t)kWaves * 64 * EPW : 0;
 }
 
 template <int W, bool TB>
@@ -101,18 +102,22 @@ __device__ __forceinline__ void wave_lds_fence() {
 // With LDS_TABLE the puzzle rows (info, root record, open bitboard) are staged in LDS once, so
 // autoresets issue no global load; the only global reads in the loop are trie records, issued
 // at on-trie transitions and first consumed at the next one.
-template <int W, bool TB, bool RAND, bool LDS_TABLE>
+// EPW = envs per wave: 64, or 32 when the batch gives fewer than two full waves per SIMD (a
+// lone wave issues a VALU op only every ~4 cycles and cannot hide its own trie-record wait;
+// two half-width waves per SIMD fill each other's gaps).
+template <int W, bool TB, bool RAND, bool LDS_TABLE, int EPW>
 __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const uint8_t* __restrict__ act,
                                                     uint64_t seed, uint64_t t0, int8_t* __restrict__ rew,
                                                     uint8_t* __restrict__ flg, int4* __restrict__ stats,
                                                     uint32_t tiled) {
-    // LDS: [I/O tiles, 3 KiB per wave][W=1 traceback: move stacks, 4 KiB per wave][puzzle rows]
+    // LDS: [I/O tiles, 3*16*EPW B per wave][W=1 traceback: move stacks, 64*EPW B per wave][rows]
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint8_t* ta = smem + wv * kTileBytes;
-    uint8_t* tr = ta + 64 * kTile;
-    uint8_t* tf = tr + 64 * kTile;
-    constexpr size_t kStackOff = kTilesLds, kTableOff = kTilesLds + stack_lds_bytes<W, TB>();
+    uint8_t* ta = smem + wv * (3 * EPW * kTile);
+    uint8_t* tr = ta + EPW * kTile;
+    uint8_t* tf = tr + EPW * kTile;
+    constexpr size_t kStackOff = tiles_lds_bytes<EPW>();
+    constexpr size_t kTableOff = kStackOff + stack_lds_bytes<W, TB, EPW>();
     PuzzleSrc<W> src{p.tab.info, p.tab.root, p.tab.open, p.tab.init, p.tab.row1};
     if constexpr (LDS_TABLE) {
         const uint32_t P = p.tab.num_puzzles;
@@ -138,17 +143,18 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
             src = PuzzleSrc<W>{linfo, lroot, lopen, p.tab.init, p.tab.row1};
         }
     }
-    const uint32_t wave_base = blockIdx.x * kBlock + wv * 64;
-    if (wave_base >= p.n) return;
+    const uint32_t wave_base = (blockIdx.x * kWaves + wv) * EPW;
+    if (wave_base >= p.n || lane >= (uint32_t)EPW) return;   // no block-level barrier after here
     const uint32_t i = wave_base + lane;
     const bool active = i < p.n;
-    const bool full = tiled && wave_base + 64 <= p.n;   // wave-uniform
+    const bool full = tiled && wave_base + EPW <= p.n;   // wave-uniform
     const size_t n = p.n;
     const uint64_t gid = p.env_offset + i;
-    const uint32_t r = lane >> 2, c = (lane & 3) * 16;   // this lane's 16-byte piece of a tile
-    using Stack = typename std::conditional<(W == 1 && TB), LdsStack, RegStack>::type;
+    constexpr uint32_t kPieces = EPW / 16;                 // 16-byte pieces per tile row
+    const uint32_t r = lane / kPieces, c = (lane % kPieces) * 16;   // this lane's piece of a tile
+    using Stack = typename std::conditional<(W == 1 && TB), LdsStack<EPW>, RegStack>::type;
     Env<W, TB, Stack> e;
-    if constexpr (W == 1 && TB) e.stk.col = smem + kStackOff + wv * kStackBytes + lane;
+    if constexpr (W == 1 && TB) e.stk.col = smem + kStackOff + wv * (64 * EPW) + lane;
     if (active) e.load(p, src, i);
     int4 acc = make_int4(0, 0, 0, 0);
     u32x4 anext = {0u, 0u, 0u, 0u};
@@ -160,7 +166,7 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
             if constexpr (!RAND) {
                 const u32x4 acur = anext;
                 if (tb + 2 * kTile <= T) anext = nt_load16(act + (size_t)(tb + kTile + r) * n + wave_base + c);
-                *reinterpret_cast<u32x4*>(ta + r * 64 + c) = acur;
+                *reinterpret_cast<u32x4*>(ta + r * EPW + c) = acur;
                 wave_lds_fence();
             }
             // 4 groups of 4 steps: each group reads its 4 actions first (one LDS wait), then
@@ -170,14 +176,14 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
                 uint32_t av[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
-                    av[j] = RAND ? uint_rand_action(seed, gid, t0 + (uint64_t)(tb + g + j)) : ta[(g + j) * 64 + lane];
+                    av[j] = RAND ? uint_rand_action(seed, gid, t0 + (uint64_t)(tb + g + j)) : ta[(g + j) * EPW + lane];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int k = g + j;
                     uint32_t f;
                     const int code = e.advance(p, src, av[j], f);
-                    tr[k * 64 + lane] = (uint8_t)code;
-                    tf[k * 64 + lane] = (uint8_t)f;
+                    tr[k * EPW + lane] = (uint8_t)code;
+                    tf[k * EPW + lane] = (uint8_t)f;
                     acc.x += code;
                     acc.y += (f & 3u) ? 1 : 0;
                     acc.z += ((f & 3u) && code == 100) ? 1 : 0;
@@ -186,8 +192,8 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
             }
             wave_lds_fence();
             const size_t o = (size_t)(tb + r) * n + wave_base + c;
-            if (rew) nt_store16(reinterpret_cast<uint8_t*>(rew) + o, *reinterpret_cast<const u32x4*>(tr + r * 64 + c));
-            if (flg) nt_store16(flg + o, *reinterpret_cast<const u32x4*>(tf + r * 64 + c));
+            if (rew) nt_store16(reinterpret_cast<uint8_t*>(rew) + o, *reinterpret_cast<const u32x4*>(tr + r * EPW + c));
+            if (flg) nt_store16(flg + o, *reinterpret_cast<const u32x4*>(tf + r * EPW + c));
             wave_lds_fence();
         } else if (active) {
             for (int k = 0; k < cnt; ++k) {
@@ -605,32 +611,40 @@ int sparc_rollout_device(void* ctx, int32_t T, const uint8_t* d_act, uint64_t se
     int4* st = reinterpret_cast<int4*>(d_stats);
     auto aligned = [](const void* q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & 15u) == 0; };
     const uint32_t tiled = (c->n % 16 == 0) && aligned(d_act) && aligned(d_rew) && aligned(d_flags);
-    // stage the puzzle rows in LDS when they fit next to the I/O tiles without costing
+    // the puzzle rows are staged in LDS when they fit next to the I/O tiles without costing
     // occupancy: budget = LDS per CU / resident workgroups per CU (256 CUs)
-    const size_t blocks = (c->n + kBlock - 1) / kBlock;
-    const size_t per_cu = (blocks + 255) / 256;
-    const size_t budget = std::min(kMaxDynLds, (size_t)160 * 1024 / (per_cu ? per_cu : 1));
+    // envs per wave: 64.  (Measured on MI355X at 65,536 envs: 32-wide waves, two per SIMD, are
+    // 1.3x slower than one full wave per SIMD — a half-empty wave costs the full issue time.)
+    const bool half = false;
     dispatch_w_tb(c->W, c->cfg.traceback, [&](auto w, auto tb) {
         constexpr int W = decltype(w)::value;
         constexpr bool TB = decltype(tb)::value;
-        const size_t base = kTilesLds + stack_lds_bytes<W, TB>();
-        const size_t tbytes = table_lds_bytes<W>(c->num_puzzles);
-        const bool lds_table = base + tbytes <= budget;
-        const size_t shm = base + (lds_table ? tbytes : 0);
-        const dim3 g = grid_for(c->n);
-        auto launch = [&](auto kern, const uint8_t* a) {
-            if (shm > 64 * 1024)
-                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-            kern<<<g, kBlock, shm, c->stream>>>(p, T, a, seed, t0, d_rew, d_flags, st, tiled);
+        auto go = [&](auto epw_c) {
+            constexpr int EPW = decltype(epw_c)::value;
+            const size_t blocks = (c->n + kWaves * EPW - 1) / (kWaves * EPW);
+            const size_t per_cu = (blocks + 255) / 256;
+            const size_t budget = std::min(kMaxDynLds, (size_t)160 * 1024 / (per_cu ? per_cu : 1));
+            const size_t base = tiles_lds_bytes<EPW>() + stack_lds_bytes<W, TB, EPW>();
+            const size_t tbytes = table_lds_bytes<W>(c->num_puzzles);
+            const bool lds_table = base + tbytes <= budget;
+            const size_t shm = base + (lds_table ? tbytes : 0);
+            const dim3 g((unsigned)blocks);
+            auto launch = [&](auto kern, const uint8_t* a) {
+                if (shm > 64 * 1024)
+                    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+                kern<<<g, kBlock, shm, c->stream>>>(p, T, a, seed, t0, d_rew, d_flags, st, tiled);
+            };
+            if (d_act) {
+                if (lds_table) launch(k_rollout<W, TB, false, true, EPW>, d_act);
+                else launch(k_rollout<W, TB, false, false, EPW>, d_act);
+            } else {
+                if (lds_table) launch(k_rollout<W, TB, true, true, EPW>, nullptr);
+                else launch(k_rollout<W, TB, true, false, EPW>, nullptr);
+            }
         };
-        if (d_act) {
-            if (lds_table) launch(k_rollout<W, TB, false, true>, d_act);
-            else launch(k_rollout<W, TB, false, false>, d_act);
-        } else {
-            if (lds_table) launch(k_rollout<W, TB, true, true>, nullptr);
-            else launch(k_rollout<W, TB, true, false>, nullptr);
-        }
+        if (half) go(std::integral_constant<int, 32>{});
+        else go(std::integral_constant<int, 64>{});
     });
     return launch_check(c);
 }

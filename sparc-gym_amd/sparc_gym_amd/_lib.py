@@ -9,7 +9,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsparc_gym_amd.so")
+LIB_PATH = os.environ.get("SPARC_DIAG_LIB") or os.path.join(_HERE, "libsparc_gym_amd.so")
 
 SPARC_OK = 0
 AUTORESET = {"none": 0, "next_step": 1}

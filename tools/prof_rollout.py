@@ -21,6 +21,9 @@ ap.add_argument("--config", default="c3")
 ap.add_argument("--envs", type=int, default=65536)
 ap.add_argument("--chunk", type=int, default=500)
 ap.add_argument("--launches", type=int, default=4)
+ap.add_argument("--rand", action="store_true", help="in-kernel counter-based actions (no action loads)")
+ap.add_argument("--no-out", action="store_true", help="do not write reward codes / flags")
+ap.add_argument("--time", action="store_true", help="print the mean launch time (HIP events)")
 a = ap.parse_args()
 sizes, full, tb = bench.CONFIGS[a.config]
 proc = process_puzzles(synthetic.make_puzzles(1024, seed=0, sizes=sizes, full_properties=full))
@@ -32,7 +35,19 @@ acts = torch.randint(0, 4, (a.launches + 1, a.chunk, a.envs), dtype=torch.uint8,
 rew = torch.empty((a.chunk, a.envs), dtype=torch.int8, device="cuda")
 flg = torch.empty((a.chunk, a.envs), dtype=torch.uint8, device="cuda")
 stats = torch.zeros((a.envs, 4), dtype=torch.int32, device="cuda")
+ms = []
 for k in range(a.launches + 1):      # first launch = warmup
-    vec.rollout(a.chunk, acts[k], stats=stats, out=(rew, flg))
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    if a.no_out:
+        vec.rollout(a.chunk, None if a.rand else acts[k], stats=stats, record=False, seed=k)
+    else:
+        vec.rollout(a.chunk, None if a.rand else acts[k], stats=stats, out=(rew, flg), seed=k)
+    e1.record()
+    ms.append((e0, e1))
 torch.cuda.synchronize()
+if a.time:
+    t = [x.elapsed_time(y) for x, y in ms[1:]]
+    print(f"rollout ms/launch {sum(t) / len(t):.4f}  env-steps/s {a.envs * a.chunk / (sum(t) / len(t) / 1e3):.4e}"
+          f"  rand={a.rand} no_out={a.no_out}")
 print("done", a.config, a.envs, a.chunk, a.launches)
