@@ -146,15 +146,21 @@ def main():
     stats = torch.zeros((n, 4), dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
 
+    vec._stream()                       # bind the context to this (torch's current) stream
+    core = vec.core
+    s_ptr = stats.data_ptr()
+
     def run(lo, hi, acts, rew_out, flag_out, events=None):
         if args.mode == "rollout":
+            # direct C-ABI calls on pre-validated buffers (vec.rollout() checks shapes per call)
+            ap, rp, fp = acts.data_ptr(), rew_out.data_ptr(), flag_out.data_ptr()
             t = lo
             while t < hi:
                 c = min(chunk, hi - t)
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if events is not None else None
                 if ev:
                     ev[0].record(stream)
-                vec.rollout(c, acts[t:t + c], stats=stats, out=(rew_out[t:t + c], flag_out[t:t + c]))
+                core.rollout_device(c, ap + t * n, rp + t * n, fp + t * n, s_ptr)
                 if ev:
                     ev[1].record(stream)
                     events.append((ev, c))
@@ -164,7 +170,7 @@ def main():
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if events is not None else None
                 if ev:
                     ev[0].record(stream)
-                vec.core.step_device(acts[t].data_ptr(), rew_out[t].data_ptr(), flag_out[t].data_ptr())
+                core.step_device(acts.data_ptr() + t * n, rew_out.data_ptr() + t * n, flag_out.data_ptr() + t * n)
                 if ev:
                     ev[1].record(stream)
                     events.append((ev, 1))
@@ -222,7 +228,8 @@ def main():
                                f"{'full property set' if full else 'base planes'}, traceback={tb}, "
                                f"max_steps={args.max_steps}, next-step autoreset, {args.puzzles} puzzles",
                    "mode": args.mode, "envs_per_gpu": n, "env_steps_per_launch": chunk if args.mode == "rollout" else 1,
-                   "parallelism": f"dp{world} (env shards, RCCL all_gather of per-env stats at end of batch)"},
+                   "parallelism": f"dp{world} (env shards, {'RCCL' if args.backend == 'nccl' else args.backend} "
+                                  f"all_gather of per-env stats at end of batch)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                      "kernel": kernel, "kernel_avg_ms": round(avg_ms, 4), "launches": len(kern_ms),

@@ -422,6 +422,7 @@ struct Env<1, TB, Stack> {
     uint32_t b, len, off, node, node_term, outcome, pending, step, pid, legal, last;
     uint32_t tgt, pflags, trie_base, trie_cnt;
     uint32_t prev_next = 0;   // traceback: move before the last one, read one step ahead
+    uint32_t solved = 0, was_reset = 0;   // this step: a +1 outcome / an autoreset (for stats)
     uint32_t bad = 0;         // sticky: a trie index was out of range (reported at store)
     uint4 rec;
 
@@ -433,11 +434,10 @@ struct Env<1, TB, Stack> {
     }
 
     __device__ __forceinline__ uint32_t legal_mask(uint32_t P) const {
-        // 32-bit window whose bit j is blocked(b - P + j); below bit 0 reads as blocked
-        const uint32_t sr = (b - P) & 63u, sl = (P - b) & 31u;
-        const uint32_t above = (uint32_t)(blk >> sr);
-        const uint32_t below = (uint32_t)(blk << sl) | ((1u << sl) - 1u);
-        const uint32_t w = ~pick(b >= P, above, below);                 // free bits (2P + 1 <= 31)
+        // 32-bit window whose bit j is blocked(b - P + j): a 64-bit rotate, because the top
+        // rows of the board (x >= x_size, all padding) are blocked and so read correctly as the
+        // out-of-lattice cells below row 0 ((x_size + 1) * pitch <= 64)
+        const uint32_t w = ~(uint32_t)__builtin_rotateright64(blk, (b - P) & 63u);   // free bits
         // up (bit P-1) and down (bit P+1) land on bits 1 and 3 with one shift and mask
         uint32_t m = (((w >> (P - 1)) & 5u) << 1) | ((w >> (2 * P)) & 1u) | ((w << 2) & 4u);
         if constexpr (TB) {
@@ -506,10 +506,9 @@ struct Env<1, TB, Stack> {
         // `action in legal` (1137): bit a of the legal mask; actions >= 4 read bit 4 (always 0)
         const uint32_t lg = rst ? 0u : legal;
         const bool moved = (lg >> (a < 4u ? a : 4u)) & 1u;
-        // neighbour offset: right +P, up -1, left -P, down +1
-        const uint32_t mag = P - ((P - 1u) & (0u - (ad & 1u)));
-        const uint32_t neg = 0u - ((ad ^ (ad >> 1)) & 1u);
-        const uint32_t nb = b + ((mag ^ neg) - neg);
+        // neighbour offset: right +P, up -1, left -P, down +1, as signed bytes of one constant
+        const uint32_t deltas = (P & 0xFFu) | (0xFFu << 8) | (((0u - P) & 0xFFu) << 16) | (1u << 24);
+        const uint32_t nb = b + (uint32_t)__builtin_amdgcn_sbfe((int)deltas, ad * 8u, 8u);
         // the only legal move onto a blocked (visited) cell is the traceback pop (1141-1166)
         const bool pop = TB & moved & (bool)((blk >> (nb & 63u)) & 1ull);
         const bool fwd = moved & !pop;                                             // 1167-1188
@@ -548,6 +547,8 @@ struct Env<1, TB, Stack> {
         const int c_done = match ? 100 : (outcome != 1 ? -100 : 0);
         const int c_move = (moved & (bool)(pflags & 1u)) ? (off == 0 ? 1 : -1) : 0;
         outcome = pick(done, pick(match | (outcome == 1), 1u, 2u), 0u);
+        solved = (uint32_t)(done & match);
+        was_reset = (uint32_t)rst;
         return done ? c_done : c_move;
     }
 

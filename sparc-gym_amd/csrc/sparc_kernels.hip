@@ -184,10 +184,17 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
                     const int code = e.advance(p, src, av[j], f);
                     tr[k * EPW + lane] = (uint8_t)code;
                     tf[k * EPW + lane] = (uint8_t)f;
-                    acc.x += code;
-                    acc.y += (f & 3u) ? 1 : 0;
-                    acc.z += ((f & 3u) && code == 100) ? 1 : 0;
-                    acc.w += (f & 64u) ? 1 : 0;
+                    if constexpr (W == 1) {   // per-step flags the W = 1 step already has
+                        acc.x += code;
+                        acc.y += (int)e.pending;
+                        acc.z += (int)e.solved;
+                        acc.w += (int)e.was_reset;
+                    } else {
+                        acc.x += code;
+                        acc.y += (f & 3u) ? 1 : 0;
+                        acc.z += ((f & 3u) && code == 100) ? 1 : 0;
+                        acc.w += (f & 64u) ? 1 : 0;
+                    }
                 }
             }
             wave_lds_fence();

@@ -41,9 +41,12 @@ def gather_stats(stats: torch.Tensor, group=None) -> torch.Tensor:
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return stats
     world = dist.get_world_size(group)
-    out = torch.empty((world * stats.shape[0],) + tuple(stats.shape[1:]), dtype=stats.dtype, device=stats.device)
-    dist.all_gather_into_tensor(out, stats.contiguous(), group=group)
-    return out
+    src = stats.contiguous()
+    if dist.get_backend(group) != "nccl":   # gloo (CPU tests / rehearsals): stage through host
+        src = src.cpu()
+    out = torch.empty((world * src.shape[0],) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
+    dist.all_gather_into_tensor(out, src, group=group)
+    return out.to(stats.device)
 
 
 def summarize(gathered: torch.Tensor) -> dict:
@@ -56,6 +59,8 @@ def max_over_ranks(seconds: float, device=None) -> float:
     """The slowest rank's time (the job's time)."""
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return seconds
+    if dist.get_backend() != "nccl":
+        device = "cpu"
     t = torch.tensor([seconds], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())

@@ -77,14 +77,12 @@ class KernelModel:
         return m
 
     def _legal_w1(self, e):
-        """Env<1, TB>::legal_mask: one window over the padded 64-bit blocked board."""
+        """Env<1, TB>::legal_mask: one rotated 32-bit window over the padded 64-bit blocked board."""
         P, M = self.t.pitch, (1 << 64) - 1
         b = e["x"] * P + e["y"]
         blk = (e["vis"] | (~e["open"] & M)) & M
-        if b >= P:
-            win = (blk >> (b - P)) & 0xFFFFFFFF
-        else:
-            win = ((blk << (P - b)) & 0xFFFFFFFF) | ((1 << (P - b)) - 1)
+        r = (b - P) & 63                       # 64-bit rotate right: padding rows wrap below row 0
+        win = ((blk >> r) | (blk << (64 - r))) & 0xFFFFFFFF
         w = ~win & 0xFFFFFFFF
         m = ((w >> (2 * P)) & 1) | (((w >> (P - 1)) & 1) << 1) | ((w & 1) << 2) | (((w >> (P + 1)) & 1) << 3)
         if self.tb and (e["len"] >= 3 or (e["len"] == 2 and not e["pflags"] & 4)):
