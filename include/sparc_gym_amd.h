@@ -162,6 +162,56 @@ int sparc_copy_state_device(void *ctx, int32_t which, void *d_out);
  *        3 step [N] u32, 4 puzzle [N] u32, 5 direction stack [2*words][N] u64 (traceback) */
 int sparc_state_ptr(void *ctx, int32_t which, void **d_ptr);
 
+/* ---- rule audit: info['rule_status'] (_validate_rules, SPaRC_Gym.py:941-950) ----------------
+ * Rule table, packed by sparc_gym_amd/puzzles.py:pack_rules from the processed puzzles, on the
+ * step table's geometry (bit x*pitch + y, `words` u64 per board).
+ *  planes      [P][SPARC_RULE_PLANES][words]: cells (odd, odd), lattice, gaps, dots, triangle
+ *              cells with count > 0 (x in 1..x_size-2, y in 1..y_size-2) and their count bits
+ *              0-2 (count clamped to 7), star, square, coloured, colour 1..8, per-cell symbol
+ *              multiplicity bits 0-2 (layers other than visited/gaps/agent/target set at a
+ *              cell), y != 0, y != y_size-1
+ *  inst_range  [P] first | count << 16 into inst (poly/ylop instances at cell centres,
+ *              _extract_poly_instances 714-734)
+ *  inst        bit | ylop << 10 | cx << 11 | cy << 14 | shape << 17
+ *  shape_range [S] first offset | count << 16 into shape_off; shape_area [S] = sum of the
+ *              shape array (722); shape_off [offsets][2] = (dx, dy) in cell units relative to
+ *              the shape's anchor (_get_offsets 840-855)
+ * Limits per puzzle: 16 ylops, 64 polys, 16 distinct poly shapes, lattice <= 15 x 15.         */
+#define SPARC_RULE_PLANES 24
+typedef struct {
+    int32_t num_puzzles;    /* must equal the loaded step table's */
+    int32_t num_inst;
+    int32_t num_shapes;
+    int32_t num_offsets;
+    const uint64_t *planes;
+    const uint32_t *inst_range;
+    const uint32_t *inst;
+    const uint32_t *shape_range;
+    const int32_t *shape_area;
+    const int8_t *shape_off;
+} sparc_rules_table;
+
+enum {
+    SPARC_RULE_REACHED_TARGET = 1 << 0,       /* _rule_reached_target 487-495        */
+    SPARC_RULE_PATH_NOT_CROSSING = 1 << 1,    /* 497-505                             */
+    SPARC_RULE_NO_GAP_VIOLATIONS = 1 << 2,    /* 507-517                             */
+    SPARC_RULE_ALL_DOTS_COLLECTED = 1 << 3,   /* 519-531                             */
+    SPARC_RULE_SQUARE_SEPARATION = 1 << 4,    /* 533-551                             */
+    SPARC_RULE_STAR_PAIRING = 1 << 5,         /* 553-619                             */
+    SPARC_RULE_TRIANGLES = 1 << 6,            /* 622-646                             */
+    SPARC_RULE_POLY_YLOP = 1 << 7,            /* 648-838                             */
+    SPARC_RULE_ALL = 1 << 8                   /* all_rules_satisfied 931-936         */
+};
+
+/* Load the rule table (host arrays, copied).  Call after sparc_load_puzzles, which drops it. */
+int sparc_load_rules(void *ctx, const sparc_rules_table *table);
+/* Audit the current state of every env: bits [N] (SPARC_RULE_*), and optionally
+ * region [N][64*words] (region id of each cell bit in the reference's numbering, 0xFF
+ * elsewhere) and fit [N] (bit r: region r holds poly/ylop instances and passes both the area
+ * check and the exact fit).  Device pointers; any output may be NULL. */
+int sparc_rules_device(void *ctx, uint16_t *d_bits, uint8_t *d_region, uint64_t *d_fit);
+int sparc_rules_host(void *ctx, uint16_t *bits, uint8_t *region, uint64_t *fit);
+
 #ifdef __cplusplus
 }
 #endif

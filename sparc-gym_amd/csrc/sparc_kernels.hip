@@ -7,6 +7,7 @@
 //              chunk ahead, reward/flags streamed out per step     (the episode loop of
 //              Final_Product.py:26-38 / llm_host.py:182-242, batched)
 //   k_obs_pack dense int32 visited / agent_location planes         (_get_obs, SPaRC_Gym.py:979)
+//   k_rules    rule audit of the current state                      (_validate_rules, 941-950)
 // No MFMA: this is integer / bitboard work, bound by latency and HBM.
 #include <hip/hip_runtime.h>
 
@@ -18,6 +19,7 @@
 #include <vector>
 
 #include "sparc_env.hpp"
+#include "sparc_rules.hpp"
 #include "sparc_gym_amd.h"
 
 using namespace sparc;
@@ -248,6 +250,27 @@ __global__ void __launch_bounds__(kBlock) k_obs_pack(Params p, int32_t* __restri
     if (agent_out) agent_out[o] = (x == (ps & 0xFFu) && y == ((ps >> 8) & 0xFFu)) ? 1 : 0;
 }
 
+template <int W>
+__global__ void __launch_bounds__(kBlock) k_rules(Params p, RulesTab rt, uint16_t* __restrict__ bits,
+                                                  uint8_t* __restrict__ region, uint64_t* __restrict__ fit) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= p.n) return;
+    const uint32_t q = p.st.pid[i];
+    if (q >= rt.num_puzzles) {
+        atomicOr(p.err, (int)kErrRuleTable);
+        return;
+    }
+    BB<W> vis;
+    for (int k = 0; k < W; ++k) vis.w[k] = p.st.vis[(size_t)k * p.n + i];
+    const uint32_t ps = p.st.pos[i];
+    uint8_t* ro = region ? region + (size_t)i * 64 * W : nullptr;
+    if (ro)
+        for (int k = 0; k < 64 * W; ++k) ro[k] = 0xFF;
+    const RuleOut<W> r = audit<W>(p, rt, vis, ps & 0xFFu, (ps >> 8) & 0xFFu, q, ro);
+    if (bits) bits[i] = (uint16_t)r.bits;
+    if (fit) fit[i] = r.fit_ok;
+}
+
 // ------------------------------------------------------------------------------ host side
 struct Ctx {
     sparc_config cfg{};
@@ -268,6 +291,15 @@ struct Ctx {
     uint8_t *s_act = nullptr, *s_flags = nullptr, *s_mask = nullptr;
     int8_t* s_rew = nullptr;
     uint32_t* s_pidx = nullptr;
+    // rule table (sparc_load_rules)
+    bool rules = false;
+    uint64_t* r_planes = nullptr;
+    uint32_t *r_inst_range = nullptr, *r_inst = nullptr, *r_shape_range = nullptr;
+    int32_t* r_shape_area = nullptr;
+    int8_t* r_shape_off = nullptr;
+    uint16_t* s_bits = nullptr;
+    uint8_t* s_region = nullptr;
+    uint64_t* s_fit = nullptr;
     std::string msg;
 };
 
@@ -397,7 +429,8 @@ int sparc_destroy(void* ctx) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->vis, c->dirs, c->pos, c->aux, c->step, c->pid, c->t_open, c->t_info, c->t_root, c->t_trie, c->t_init, c->t_row1,
-                    c->err, c->s_act, c->s_flags, c->s_mask, c->s_rew, c->s_pidx};
+                    c->err, c->s_act, c->s_flags, c->s_mask, c->s_rew, c->s_pidx, c->r_planes, c->r_inst_range,
+                    c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off, c->s_bits, c->s_region, c->s_fit};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->own) (void)hipStreamDestroy(c->own);
@@ -429,6 +462,8 @@ int sparc_sync(void* ctx) {
     if (e) {
         HIPCHK(c, hipMemset(c->err, 0, sizeof(int32_t)));
         if (e & 2) return fail(c, SPARC_E_STATE, "device-side trie node out of range (state corrupted)");
+        if (e & 4) return fail(c, SPARC_E_STATE, "rule audit: exact-fit search exceeded 2^26 nodes");
+        if (e & 8) return fail(c, SPARC_E_STATE, "rule audit: env puzzle index outside the rule table");
         return fail(c, SPARC_E_INVALID, "device-side puzzle index out of range in a reset");
     }
     return SPARC_OK;
@@ -545,6 +580,7 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
     c->num_puzzles = (uint32_t)t->num_puzzles;
     c->num_nodes = (uint32_t)t->num_nodes;
     c->loaded = true;
+    c->rules = false;       // the rule table indexes the old puzzles
     c->has_state = false;   // old state may point at puzzles that no longer exist
     return SPARC_OK;
 }
@@ -668,6 +704,110 @@ int sparc_obs_pack_device(void* ctx, int32_t* d_vis, int32_t* d_agent, int32_t x
     else if (c->W == 2) k_obs_pack<2><<<g, kBlock, 0, c->stream>>>(p, d_vis, d_agent, xd, yd);
     else k_obs_pack<4><<<g, kBlock, 0, c->stream>>>(p, d_vis, d_agent, xd, yd);
     return launch_check(c);
+}
+
+int sparc_load_rules(void* ctx, const sparc_rules_table* t) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    int rc = check_ctx(c, false);
+    if (rc) return rc;
+    if (!t || !t->planes || !t->inst_range) return fail(c, SPARC_E_INVALID, "null argument");
+    if ((uint32_t)t->num_puzzles != c->num_puzzles)
+        return fail(c, SPARC_E_INVALID, "rule table puzzle count differs from the loaded puzzle table");
+    if (t->num_inst < 0 || t->num_shapes < 0 || t->num_offsets < 0 || t->num_offsets > 0xFFFF ||
+        t->num_shapes >= (1 << 15) || (t->num_inst && !t->inst) ||
+        (t->num_shapes && (!t->shape_range || !t->shape_area)) || (t->num_offsets && !t->shape_off))
+        return fail(c, SPARC_E_INVALID, "bad rule table sizes");
+    const int W = c->W;
+    const size_t P = (size_t)t->num_puzzles;
+    std::vector<uint4> info(P);
+    HIPCHK(c, hipMemcpy(info.data(), c->t_info, sizeof(uint4) * P, hipMemcpyDeviceToHost));
+    for (int sh = 0; sh < t->num_shapes; ++sh) {
+        const uint32_t o0 = t->shape_range[sh] & 0xFFFFu, n = t->shape_range[sh] >> 16;
+        if (o0 + n > (uint32_t)t->num_offsets) return fail(c, SPARC_E_INVALID, "shape offsets out of range");
+    }
+    for (size_t q = 0; q < P; ++q) {
+        const uint32_t X = info[q].x & 0xFFu, Y = (info[q].x >> 8) & 0xFFu;
+        const uint32_t f = t->inst_range[q] & 0xFFFFu, n = t->inst_range[q] >> 16;
+        char m[160];
+        if (X > 15 || Y > 15) {
+            snprintf(m, sizeof m, "puzzle %zu: the rule audit supports lattices up to 15x15", q);
+            return fail(c, SPARC_E_INVALID, m);
+        }
+        if ((uint64_t)f + n > (uint64_t)t->num_inst) return fail(c, SPARC_E_INVALID, "instance range out of bounds");
+        int ny = 0, np = 0, nd = 0;
+        uint32_t ds[kFitShapes + 1];
+        for (uint32_t k = 0; k < n; ++k) {
+            const uint32_t e = t->inst[f + k], b = e & 0x3FFu, sh = e >> 17;
+            if (b >= 64u * W || sh >= (uint32_t)t->num_shapes) return fail(c, SPARC_E_INVALID, "bad instance");
+            if ((e >> 10) & 1u) { ++ny; continue; }
+            ++np;
+            int j = 0;
+            while (j < nd && ds[j] != sh) ++j;
+            if (j == nd && nd <= kFitShapes) ds[nd++] = sh;
+        }
+        if (ny > kFitYlops || np > kFitDepth || nd > kFitShapes) {
+            snprintf(m, sizeof m, "puzzle %zu: %d ylops / %d polys / %d poly shapes exceed 16 / 64 / 16", q, ny, np, nd);
+            return fail(c, SPARC_E_INVALID, m);
+        }
+    }
+    void* old[] = {c->r_planes, c->r_inst_range, c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off};
+    for (void* b : old)
+        if (b) HIPCHK(c, hipFree(b));
+    c->r_planes = nullptr; c->r_inst_range = nullptr; c->r_inst = nullptr;
+    c->r_shape_range = nullptr; c->r_shape_area = nullptr; c->r_shape_off = nullptr;
+    c->rules = false;
+    const size_t np_ = P * RP_COUNT * W;
+    const size_t ni = std::max<size_t>(1, t->num_inst), ns = std::max<size_t>(1, t->num_shapes),
+                 no = std::max<size_t>(1, t->num_offsets);
+    HIPCHK(c, hipMalloc(&c->r_planes, sizeof(uint64_t) * np_));
+    HIPCHK(c, hipMalloc(&c->r_inst_range, sizeof(uint32_t) * P));
+    HIPCHK(c, hipMalloc(&c->r_inst, sizeof(uint32_t) * ni));
+    HIPCHK(c, hipMalloc(&c->r_shape_range, sizeof(uint32_t) * ns));
+    HIPCHK(c, hipMalloc(&c->r_shape_area, sizeof(int32_t) * ns));
+    HIPCHK(c, hipMalloc(&c->r_shape_off, 2 * no));
+    HIPCHK(c, hipMemcpy(c->r_planes, t->planes, sizeof(uint64_t) * np_, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->r_inst_range, t->inst_range, sizeof(uint32_t) * P, hipMemcpyHostToDevice));
+    if (t->num_inst) HIPCHK(c, hipMemcpy(c->r_inst, t->inst, sizeof(uint32_t) * t->num_inst, hipMemcpyHostToDevice));
+    if (t->num_shapes) {
+        HIPCHK(c, hipMemcpy(c->r_shape_range, t->shape_range, sizeof(uint32_t) * t->num_shapes, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(c->r_shape_area, t->shape_area, sizeof(int32_t) * t->num_shapes, hipMemcpyHostToDevice));
+    }
+    if (t->num_offsets) HIPCHK(c, hipMemcpy(c->r_shape_off, t->shape_off, 2 * (size_t)t->num_offsets, hipMemcpyHostToDevice));
+    c->rules = true;
+    return SPARC_OK;
+}
+
+int sparc_rules_device(void* ctx, uint16_t* d_bits, uint8_t* d_region, uint64_t* d_fit) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    int rc = check_ctx(c, true);
+    if (rc) return rc;
+    if (!c->rules) return fail(c, SPARC_E_STATE, "sparc_load_rules has not been called");
+    const Params p = make_params(c);
+    const RulesTab rt{c->r_planes, c->r_inst_range, c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off,
+                      c->num_puzzles};
+    const dim3 g = grid_for(c->n);
+    if (c->W == 1) k_rules<1><<<g, kBlock, 0, c->stream>>>(p, rt, d_bits, d_region, d_fit);
+    else if (c->W == 2) k_rules<2><<<g, kBlock, 0, c->stream>>>(p, rt, d_bits, d_region, d_fit);
+    else k_rules<4><<<g, kBlock, 0, c->stream>>>(p, rt, d_bits, d_region, d_fit);
+    return launch_check(c);
+}
+
+int sparc_rules_host(void* ctx, uint16_t* bits, uint8_t* region, uint64_t* fit) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    int rc = check_ctx(c, true);
+    if (rc) return rc;
+    const size_t n = c->n, rb = n * 64 * c->W;
+    if (!c->s_bits) {
+        HIPCHK(c, hipMalloc(&c->s_bits, 2 * n));
+        HIPCHK(c, hipMalloc(&c->s_region, rb));
+        HIPCHK(c, hipMalloc(&c->s_fit, 8 * n));
+    }
+    rc = sparc_rules_device(c, c->s_bits, region ? c->s_region : nullptr, fit ? c->s_fit : nullptr);
+    if (rc) return rc;
+    if (bits) HIPCHK(c, hipMemcpyAsync(bits, c->s_bits, 2 * n, hipMemcpyDeviceToHost, c->stream));
+    if (region) HIPCHK(c, hipMemcpyAsync(region, c->s_region, rb, hipMemcpyDeviceToHost, c->stream));
+    if (fit) HIPCHK(c, hipMemcpyAsync(fit, c->s_fit, 8 * n, hipMemcpyDeviceToHost, c->stream));
+    return sparc_sync(c);
 }
 
 int sparc_read_state(void* ctx, const sparc_state_host* o) {

@@ -1,0 +1,321 @@
+// sparc_rules.hpp — per-lane rule audit for gfx950 (device code).
+//
+// Restates SPaRC_Gym._validate_rules (SPaRC_Gym.py:941-950) for one env per lane, on the
+// same bitboards as the step (bit x*pitch + y, W words):
+//   _compute_regions (423-454)  regions = connected components of {cell centres} ∪ {free
+//                               lattice points}, free = in lattice, not a gap, not on the
+//                               path.  Found by bitboard flood fill from the lowest unassigned
+//                               cell (the reference's x-major scan order gives the region ids).
+//   _collect_region_symbols     per-cell multiplicity (symbol layers set at the cell) and colour
+//   (456-481)                   as bit-planes: counts are popcounts of region ∧ plane.
+//   reached_target (487-495)    agent == target
+//   path_not_crossing (497-505) always true: a move only enters an unvisited point and a pop
+//                               removes the last one, so the path never repeats a point
+//   no_gap_violations (507-517) visited ∧ gaps == ∅ (the path's point set is `visited`)
+//   all_dots_collected (519-531) dots ∧ ¬visited == ∅
+//   square_color_separation     per region: at most one non-zero square colour
+//   (533-551)
+//   star_pairing_exact (553-619) per region: no colourless star; for each star colour c the
+//                               region holds exactly 2 symbol occurrences of colour c
+//   triangles_edge_count        per triangle cell with count > 0: path points among its 4
+//   (622-646)                   neighbours == count, as a bit-sliced 4-input popcount
+//   poly_ylop_area (648-709)    per region holding instances: area == Σpoly − Σylop, then the
+//                               exact-fit search of 736-838 (exists / not: the same answer for
+//                               any complete search order, so identical ylops are placed in
+//                               non-decreasing anchor order and polys by distinct shape)
+// Output bit k = RULE k in the order of _run_rule_validators (899-939), bit 8 = all.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sparc_env.hpp"
+
+namespace sparc {
+
+constexpr uint32_t kErrRuleSearch = 4, kErrRuleTable = 8;
+// rule-plane indices of include/sparc_gym_amd.h (SPARC_RULE_PLANES)
+enum : uint32_t {
+    RP_CELLS = 0, RP_LATTICE, RP_GAPS, RP_DOTS, RP_TRI, RP_TRI0, RP_TRI1, RP_TRI2, RP_STAR, RP_SQUARE,
+    RP_COLORED, RP_COL1, RP_M0 = RP_COL1 + 8, RP_M1, RP_M2, RP_NOTFIRST, RP_NOTLAST, RP_COUNT
+};
+constexpr int kFitCells = 64;     // cell grid of the exact fit (15 x 15 lattice: 7 x 7 = 49)
+constexpr int kFitYlops = 16;     // per puzzle limits, validated by the loader
+constexpr int kFitShapes = 16;
+constexpr int kFitDepth = 64;
+constexpr uint32_t kFitCap = 1u << 26;   // search nodes before a loud failure (kErrRuleSearch)
+
+struct RulesTab {
+    const uint64_t* __restrict__ planes;      // [P][RP_COUNT][W]
+    const uint32_t* __restrict__ inst_range;  // [P] first | count << 16
+    const uint32_t* __restrict__ inst;        // bit | ylop << 10 | cx << 11 | cy << 14 | shape << 17
+    const uint32_t* __restrict__ shape_range; // [S] first offset | count << 16
+    const int32_t* __restrict__ shape_area;   // [S] sum of the shape array (the area of 722-723)
+    const int8_t* __restrict__ shape_off;     // [offsets][2] (dcx, dcy) in cell units
+    uint32_t num_puzzles;
+};
+
+template <int W>
+struct BB {
+    uint64_t w[W];
+    __device__ __forceinline__ static BB zero() { BB r; for (int k = 0; k < W; ++k) r.w[k] = 0; return r; }
+    __device__ __forceinline__ static BB load(const uint64_t* p) { BB r; for (int k = 0; k < W; ++k) r.w[k] = p[k]; return r; }
+    __device__ __forceinline__ BB operator&(const BB& o) const { BB r; for (int k = 0; k < W; ++k) r.w[k] = w[k] & o.w[k]; return r; }
+    __device__ __forceinline__ BB operator|(const BB& o) const { BB r; for (int k = 0; k < W; ++k) r.w[k] = w[k] | o.w[k]; return r; }
+    __device__ __forceinline__ BB operator^(const BB& o) const { BB r; for (int k = 0; k < W; ++k) r.w[k] = w[k] ^ o.w[k]; return r; }
+    __device__ __forceinline__ BB andnot(const BB& o) const { BB r; for (int k = 0; k < W; ++k) r.w[k] = w[k] & ~o.w[k]; return r; }
+    __device__ __forceinline__ bool any() const { uint64_t a = 0; for (int k = 0; k < W; ++k) a |= w[k]; return a != 0; }
+    __device__ __forceinline__ bool operator==(const BB& o) const {
+        uint64_t a = 0; for (int k = 0; k < W; ++k) a |= w[k] ^ o.w[k]; return a == 0;
+    }
+    __device__ __forceinline__ int popc() const { int s = 0; for (int k = 0; k < W; ++k) s += __popcll(w[k]); return s; }
+    __device__ __forceinline__ bool test(uint32_t b) const { return (w[b >> 6] >> (b & 63)) & 1ull; }
+    __device__ __forceinline__ void set(uint32_t b) { w[b >> 6] |= 1ull << (b & 63); }
+    // lowest set bit index (requires any())
+    __device__ __forceinline__ uint32_t lowest() const {
+        for (int k = 0; k < W; ++k)
+            if (w[k]) return 64u * k + (uint32_t)__ffsll((long long)w[k]) - 1u;
+        return 0;
+    }
+    // toward higher bit indices by s (0 < s < 64)
+    __device__ __forceinline__ BB shl(uint32_t s) const {
+        BB r;
+        for (int k = W - 1; k >= 0; --k) r.w[k] = (w[k] << s) | (k ? w[k - 1] >> (64 - s) : 0);
+        return r;
+    }
+    __device__ __forceinline__ BB shr(uint32_t s) const {
+        BB r;
+        for (int k = 0; k < W; ++k) r.w[k] = (w[k] >> s) | (k + 1 < W ? w[k + 1] << (64 - s) : 0);
+        return r;
+    }
+};
+
+struct FitIn {
+    const RulesTab* rt;
+    uint32_t first, count;   // the puzzle's instance range
+    uint32_t CX, CY;         // cell grid
+};
+
+// ---------------------------------------------------------------- exact fit (736-838)
+__device__ __forceinline__ bool fit_place(int8_t* g, const RulesTab& rt, uint32_t shape, int a, uint32_t CX,
+                                          uint32_t CY, int sign) {
+    const uint32_t sr = rt.shape_range[shape];
+    const uint32_t o0 = sr & 0xFFFFu, n = sr >> 16;
+    const int ax = a / (int)CY, ay = a - ax * (int)CY;
+    for (uint32_t k = 0; k < n; ++k) {   // _try_place_polys: all targets in bounds first
+        const int tx = ax + rt.shape_off[2 * (o0 + k)], ty = ay + rt.shape_off[2 * (o0 + k) + 1];
+        if (tx < 0 || tx >= (int)CX || ty < 0 || ty >= (int)CY) return false;
+    }
+    for (uint32_t k = 0; k < n; ++k) {
+        const int tx = ax + rt.shape_off[2 * (o0 + k)], ty = ay + rt.shape_off[2 * (o0 + k) + 1];
+        g[tx * (int)CY + ty] += (int8_t)sign;
+    }
+    return true;
+}
+
+__device__ __forceinline__ void fit_unplace(int8_t* g, const RulesTab& rt, uint32_t shape, int a, uint32_t CY,
+                                            int sign) {
+    const uint32_t sr = rt.shape_range[shape];
+    const uint32_t o0 = sr & 0xFFFFu, n = sr >> 16;
+    const int ax = a / (int)CY, ay = a - ax * (int)CY;
+    for (uint32_t k = 0; k < n; ++k) {
+        const int tx = ax + rt.shape_off[2 * (o0 + k)], ty = ay + rt.shape_off[2 * (o0 + k) + 1];
+        g[tx * (int)CY + ty] -= (int8_t)sign;
+    }
+}
+
+// _polyfit_region_exact with area already equal (so net = area > 0 and the grid starts at -1
+// on the region's cells).  region_cell(k) tells whether cell k (= cx*CY + cy) is in the region.
+template <int W>
+__device__ __noinline__ bool exact_fit(const FitIn& in, const BB<W>& Rc, uint32_t pitch, int32_t* err) {
+    const RulesTab& rt = *in.rt;
+    const int NC = (int)(in.CX * in.CY);
+    int8_t g[kFitCells];
+    for (int k = 0; k < NC; ++k) {
+        const uint32_t cx = (uint32_t)k / in.CY, cy = (uint32_t)k - cx * in.CY;
+        g[k] = Rc.test((2 * cx + 1) * pitch + 2 * cy + 1) ? (int8_t)-1 : (int8_t)0;
+    }
+    uint32_t ysh[kFitYlops], dsh[kFitShapes];
+    int cnt[kFitShapes];
+    int ny = 0, nd = 0, np = 0;
+    for (uint32_t k = 0; k < in.count; ++k) {
+        const uint32_t e = rt.inst[in.first + k];
+        if (!Rc.test(e & 0x3FFu)) continue;
+        const uint32_t sh = e >> 17;
+        if ((e >> 10) & 1u) {                 // ylop, kept sorted by shape (insertion sort)
+            int j = ny++;
+            while (j > 0 && ysh[j - 1] > sh) { ysh[j] = ysh[j - 1]; --j; }
+            ysh[j] = sh;
+        } else {
+            int j = 0;
+            while (j < nd && dsh[j] != sh) ++j;
+            if (j == nd) { dsh[nd] = sh; cnt[nd] = 0; ++nd; }
+            ++cnt[j];
+            ++np;
+        }
+    }
+    int cur[kFitYlops + kFitDepth + 1];
+    int pat[kFitDepth + 1];
+    const int LMAX = ny + np;
+    int L = 0;
+    cur[0] = -1;
+    uint32_t iters = 0;
+    while (true) {
+        if (++iters > kFitCap) { atomicOr(err, (int)kErrRuleSearch); return false; }
+        if (L < ny) {                                            // _polyfit_place_ylops
+            int a = cur[L];
+            if (a >= 0) fit_unplace(g, rt, ysh[L], a, in.CY, -1);
+            a = a < 0 ? ((L > 0 && ysh[L] == ysh[L - 1]) ? cur[L - 1] : 0) : a + 1;
+            while (a < NC && !fit_place(g, rt, ysh[L], a, in.CX, in.CY, -1)) ++a;
+            if (a >= NC) {
+                cur[L] = -1;
+                if (L == 0) return false;
+                --L;
+                continue;
+            }
+            cur[L] = a;
+            cur[++L] = -1;
+            continue;
+        }
+        const int lv = L - ny;                                   // _polyfit_place_polys
+        int j = cur[L];
+        if (j < 0) {
+            bool pos = false, neg = false;
+            int t = -1;
+            for (int k = 0; k < NC; ++k) {
+                pos |= g[k] > 0;
+                if (g[k] < 0 && t < 0) t = k;
+            }
+            neg = t >= 0;
+            bool done = false, ok = false;
+            if (pos) done = true;                                // any(grid > 0): False
+            else if (L == LMAX) { done = true; ok = !neg; }       // no polys left
+            else if (!neg) { done = true; ok = true; }           // no negative cell: True
+            if (done) {
+                if (ok) return true;
+                if (L == 0) return false;
+                --L;
+                continue;
+            }
+            pat[lv] = t;
+        } else {
+            fit_unplace(g, rt, dsh[j], pat[lv], in.CY, +1);
+            ++cnt[j];
+        }
+        ++j;
+        while (j < nd && (cnt[j] == 0 || !fit_place(g, rt, dsh[j], pat[lv], in.CX, in.CY, +1))) ++j;
+        if (j >= nd) {
+            cur[L] = -1;
+            if (L == 0) return false;
+            --L;
+            continue;
+        }
+        --cnt[j];
+        cur[L] = j;
+        cur[++L] = -1;
+    }
+}
+
+// ---------------------------------------------------------------- the audit
+template <int W>
+struct RuleOut {
+    uint32_t bits;
+    uint64_t fit_ok;   // bit r: region r held instances and passed the area check and the fit
+};
+
+// vis: path points; x, y: agent; q: puzzle.  region_out (may be null): region id per bit.
+template <int W>
+__device__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const BB<W>& vis, uint32_t x, uint32_t y,
+                            uint32_t q, uint8_t* region_out) {
+    const uint64_t* pl = rt.planes + (size_t)q * RP_COUNT * W;
+    const uint4 inf = p.tab.info[q];
+    const uint32_t X = inf.x & 0xFFu, Y = (inf.x >> 8) & 0xFFu;
+    const uint32_t tx = inf.y & 0xFFu, ty = (inf.y >> 8) & 0xFFu;
+    const uint32_t P = p.pitch;
+    const BB<W> cells = BB<W>::load(pl + RP_CELLS * W);
+    const BB<W> lattice = BB<W>::load(pl + RP_LATTICE * W);
+    const BB<W> gaps = BB<W>::load(pl + RP_GAPS * W);
+    const BB<W> nfirst = BB<W>::load(pl + RP_NOTFIRST * W), nlast = BB<W>::load(pl + RP_NOTLAST * W);
+    const BB<W> allowed = lattice.andnot(gaps | vis) | cells;
+    const uint32_t ir = rt.inst_range[q];
+    const FitIn fin{&rt, ir & 0xFFFFu, ir >> 16, (X - 1) / 2, (Y - 1) / 2};
+
+    bool sq_ok = true, star_ok = true, poly_ok = true;
+    uint64_t fit_ok = 0;
+    BB<W> remaining = cells;
+    uint32_t rid = 0;
+    while (remaining.any()) {
+        BB<W> R = BB<W>::zero();
+        R.set(remaining.lowest());
+        while (true) {                                           // flood fill (BFS 431-452)
+            BB<W> N = R | (R.shl(1) & nfirst) | (R.shr(1) & nlast) | R.shl(P) | R.shr(P);
+            N = N & allowed;
+            if (N == R) break;
+            R = N;
+        }
+        const BB<W> Rc = R & cells;
+        remaining = remaining.andnot(Rc);
+        if (region_out) {
+            BB<W> t = Rc;
+            while (t.any()) {
+                const uint32_t b = t.lowest();
+                region_out[b] = (uint8_t)rid;
+                t.w[b >> 6] &= t.w[b >> 6] - 1;
+            }
+        }
+        // squares: at most one non-zero colour (533-551)
+        const BB<W> sq = Rc & BB<W>::load(pl + RP_SQUARE * W);
+        if (sq.any()) {
+            int ncol = 0;
+            for (int c = 0; c < 8; ++c) ncol += (sq & BB<W>::load(pl + (RP_COL1 + c) * W)).any();
+            sq_ok &= ncol <= 1;
+        }
+        // stars (553-619)
+        const BB<W> st = Rc & BB<W>::load(pl + RP_STAR * W);
+        if (st.any()) {
+            star_ok &= !st.andnot(BB<W>::load(pl + RP_COLORED * W)).any();
+            const BB<W> m0 = BB<W>::load(pl + RP_M0 * W), m1 = BB<W>::load(pl + RP_M1 * W),
+                        m2 = BB<W>::load(pl + RP_M2 * W);
+            for (int c = 0; c < 8; ++c) {
+                const BB<W> col = Rc & BB<W>::load(pl + (RP_COL1 + c) * W);
+                if (!(st & col).any()) continue;
+                const int tot = (col & m0).popc() + 2 * (col & m1).popc() + 4 * (col & m2).popc();
+                star_ok &= tot == 2;
+            }
+        }
+        // poly / ylop (648-709)
+        int pa = 0, ya = 0;
+        bool has = false;
+        for (uint32_t k = 0; k < fin.count; ++k) {
+            const uint32_t e = rt.inst[fin.first + k];
+            if (!Rc.test(e & 0x3FFu)) continue;
+            has = true;
+            const int a = rt.shape_area[e >> 17];
+            if ((e >> 10) & 1u) ya += a; else pa += a;
+        }
+        if (has) {
+            bool ok = Rc.popc() == pa - ya;
+            if (ok) ok = exact_fit<W>(fin, Rc, P, p.err);
+            if (ok) fit_ok |= 1ull << (rid & 63);
+            poly_ok &= ok;
+        }
+        ++rid;
+    }
+    // triangles: bit-sliced count of path neighbours (x±1: ±P, y±1: ±1)
+    const BB<W> a = vis.shr(P), b = vis.shl(P), c = vis.shr(1), d = vis.shl(1);
+    const BB<W> s1 = a ^ b, c1 = a & b, s2 = c ^ d, c2 = c & d;
+    const BB<W> n0 = s1 ^ s2, k0 = s1 & s2, n1 = c1 ^ c2 ^ k0, n2 = c1 & c2;
+    const BB<W> bad = BB<W>::load(pl + RP_TRI * W) &
+                      ((n0 ^ BB<W>::load(pl + RP_TRI0 * W)) | (n1 ^ BB<W>::load(pl + RP_TRI1 * W)) |
+                       (n2 ^ BB<W>::load(pl + RP_TRI2 * W)));
+    const bool tri_ok = !bad.any();
+    const bool reached = x == tx && y == ty;
+    const bool gap_ok = !(gaps & vis).any();
+    const bool dot_ok = !BB<W>::load(pl + RP_DOTS * W).andnot(vis).any();
+    uint32_t bits = (uint32_t)reached | 2u | ((uint32_t)gap_ok << 2) | ((uint32_t)dot_ok << 3) |
+                    ((uint32_t)sq_ok << 4) | ((uint32_t)star_ok << 5) | ((uint32_t)tri_ok << 6) |
+                    ((uint32_t)poly_ok << 7);
+    bits |= (uint32_t)((bits & 0xFFu) == 0xFFu) << 8;
+    return RuleOut<W>{bits, fit_ok};
+}
+
+}  // namespace sparc

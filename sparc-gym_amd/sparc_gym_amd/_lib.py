@@ -33,6 +33,12 @@ class SparcStateHost(ctypes.Structure):
                 ("puzzle", c_void_p), ("outcome", c_void_p), ("pending", c_void_p), ("visited", c_void_p)]
 
 
+class SparcRulesTable(ctypes.Structure):
+    _fields_ = [("num_puzzles", ctypes.c_int32), ("num_inst", ctypes.c_int32), ("num_shapes", ctypes.c_int32),
+                ("num_offsets", ctypes.c_int32), ("planes", c_void_p), ("inst_range", c_void_p), ("inst", c_void_p),
+                ("shape_range", c_void_p), ("shape_area", c_void_p), ("shape_off", c_void_p)]
+
+
 _SIGS = {
     "sparc_abi_version": ([], c_int32),
     "sparc_last_error": ([c_void_p], ctypes.c_char_p),
@@ -52,6 +58,9 @@ _SIGS = {
     "sparc_read_state": ([c_void_p, ctypes.POINTER(SparcStateHost)], c_int32),
     "sparc_state_ptr": ([c_void_p, c_int32, ctypes.POINTER(c_void_p)], c_int32),
     "sparc_copy_state_device": ([c_void_p, c_int32, c_void_p], c_int32),
+    "sparc_load_rules": ([c_void_p, ctypes.POINTER(SparcRulesTable)], c_int32),
+    "sparc_rules_device": ([c_void_p, c_void_p, c_void_p, c_void_p], c_int32),
+    "sparc_rules_host": ([c_void_p, c_void_p, c_void_p, c_void_p], c_int32),
 }
 EXPORTS = tuple(_SIGS)
 

@@ -10,7 +10,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from .puzzles import PuzzleTable
+from .puzzles import PuzzleTable, RulesTable
 
 INT32_MAX = 2**31 - 1
 
@@ -46,6 +46,36 @@ class SparcCore:
                                   trie.ctypes.data if len(trie) else None)
         self._check(self.lib.sparc_load_puzzles(self.ctx, ctypes.byref(t)))
         self.table = table
+
+    def load_rules(self, rt: RulesTable):
+        """Upload the rule-audit table (puzzles.pack_rules) for the loaded puzzles."""
+        planes = np.ascontiguousarray(rt.planes, np.uint64)
+        rng = np.ascontiguousarray(rt.inst_range, np.uint32)
+        inst = np.ascontiguousarray(rt.inst, np.uint32)
+        sr = np.ascontiguousarray(rt.shape_range, np.uint32)
+        sa = np.ascontiguousarray(rt.shape_area, np.int32)
+        so = np.ascontiguousarray(rt.shape_off, np.int8)
+        t = _lib.SparcRulesTable(len(rng), len(inst), len(sr), len(so), planes.ctypes.data, rng.ctypes.data,
+                                 inst.ctypes.data if len(inst) else None, sr.ctypes.data if len(sr) else None,
+                                 sa.ctypes.data if len(sa) else None, so.ctypes.data if len(so) else None)
+        self._check(self.lib.sparc_load_rules(self.ctx, ctypes.byref(t)))
+        self.rules = rt
+
+    def rules_host(self, region=False, fit=False):
+        """Rule audit of every env's current state: dict of bits [N] uint16 (+ region
+        [N][64*words] uint8, fit [N] uint64 when asked)."""
+        n, W = self.num_envs, self.table.words
+        out = {"bits": np.empty(n, np.uint16)}
+        if region:
+            out["region"] = np.empty((n, 64 * W), np.uint8)
+        if fit:
+            out["fit"] = np.empty(n, np.uint64)
+        self._check(self.lib.sparc_rules_host(self.ctx, _ptr(out["bits"]), _ptr(out.get("region")),
+                                              _ptr(out.get("fit"))))
+        return out
+
+    def rules_device(self, d_bits, d_region=None, d_fit=None):
+        self._check(self.lib.sparc_rules_device(self.ctx, d_bits, d_region, d_fit))
 
     def close(self):
         if getattr(self, "ctx", None) is not None and self.ctx.value:

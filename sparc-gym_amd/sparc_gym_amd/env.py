@@ -12,7 +12,10 @@ Differences (documented in DESIGN.md):
   still honoured when ``puzzles`` is None.
 * Every reset restores pristine planes (the reference's first load of a puzzle); the reference
   aliases the planes across re-loads (SPaRC_Gym.py:149-151).
-* ``info['rule_status']`` (the info-only rule audit, 941-950) is ``{}``: out of scope.
+* ``info['rule_status']`` (the rule audit, 941-950) is computed by the k_rules kernel and laid
+  out in the reference's dict shape by ``rules.rule_status``; ``rule_status=False`` skips it
+  (then ``{}``).  After ``__init__`` (before any reset) it describes the loaded state with the
+  start point visited; the reference audits once before marking it (182-185).
 * ``render_mode='human'/'llm'`` needs pygame, which is not available: raises.
 """
 from __future__ import annotations
@@ -23,7 +26,8 @@ from collections import OrderedDict
 import numpy as np
 
 from .core import SparcCore
-from .puzzles import pack_table, process_puzzles
+from .puzzles import pack_rules, pack_table, process_puzzles
+from .rules import region_map_of, rule_status as _rule_status
 from .spaces import Box, Dict, Discrete, Env, Text
 
 _REWARD = {0: 0, 1: 0.01, -1: -0.01, 100: 1, -100: -1}   # code -> the reference's Python value
@@ -56,7 +60,7 @@ class SPaRC_Gym(Env):
     metadata = {"render_modes": ["human", "llm"], "render_fps": 30}
 
     def __init__(self, df_name="lkaesberg/SPaRC", df_split="all", df_set="test", render_mode=None,
-                 observation="new", traceback=False, max_steps=2000, puzzles=None, device=0):
+                 observation="new", traceback=False, max_steps=2000, puzzles=None, device=0, rule_status=True):
         self.render_mode = render_mode
         self.observation = observation
         self.traceback = traceback
@@ -71,8 +75,12 @@ class SPaRC_Gym(Env):
             raise ValueError("No valid dataframe provided")                          # 86-87
         self.puzzles = process_puzzles(df, observation)
         self._core = SparcCore(pack_table(self.puzzles), 1, traceback, max_steps, "none", device)
+        self._audit = bool(rule_status)
+        if self._audit:
+            self._core.load_rules(pack_rules(self.puzzles, self._core.table))
         self._legal = 0
         self._load_puzzle(self.current_puzzle_index)
+        self._validate_rules()                                                       # 182
 
     # ------------------------------------------------------------------ loading
     def _load_puzzle(self, index):
@@ -198,11 +206,24 @@ class SPaRC_Gym(Env):
     def _build_json_obs(self):
         return json.dumps(self.observ, separators=(",", ":"))
 
+    def _validate_rules(self, terminated=False, truncated=False):
+        """_validate_rules (SPaRC_Gym.py:941-950): the audit runs in the k_rules kernel."""
+        if not self._audit:
+            self.rule_status = {}
+            return self.rule_status
+        r = self._core.rules_host(region=True, fit=True)
+        rmap = region_map_of(r["region"][0], self.x_size, self.y_size, self._core.table.pitch)
+        self.rule_status = _rule_status(self.puzzles[self.current_puzzle_index], self.obs_array, self.path,
+                                        self._agent_location, self._target_location, r["bits"][0], rmap,
+                                        r["fit"][0], terminated, truncated)
+        return self.rule_status
+
     def _get_legal_actions(self):
         return [a for a in range(4) if (self._legal >> a) & 1]
 
     def _get_info(self):
-        """SPaRC_Gym.py:994-1022 (rule_status out of scope: {})."""
+        """SPaRC_Gym.py:994-1022."""
+        self._validate_rules(terminated=False, truncated=False)
         return {"solution_count": self.solution_count,
                 "difficulty": self.difficulty,
                 "grid_x_size": self.x_size,

@@ -278,3 +278,128 @@ def pack_table(puzzles, pitch=None, words=None):
             base += len(nodes)
     trie = np.concatenate(tries) if tries else np.zeros((0, 4), np.uint32)
     return PuzzleTable(open_, info, np.ascontiguousarray(trie), pitch, words, x_max, y_max)
+
+
+# ----------------------------------------------------------------------------------- rule audit
+RULE_PLANES = 24   # SPARC_RULE_PLANES
+(RP_CELLS, RP_LATTICE, RP_GAPS, RP_DOTS, RP_TRI, RP_TRI0, RP_TRI1, RP_TRI2, RP_STAR, RP_SQUARE,
+ RP_COLORED) = range(11)
+RP_COL1, RP_M0, RP_M1, RP_M2, RP_NOTFIRST, RP_NOTLAST = 11, 19, 20, 21, 22, 23
+RULE_SKIP_LAYERS = ("visited", "gaps", "agent_location", "target_location")   # SPaRC_Gym.py:466
+
+
+@dataclass
+class RulesTable:
+    """Rule-audit table (layout: include/sparc_gym_amd.h, sparc_rules_table)."""
+    planes: np.ndarray       # uint64 [P][RULE_PLANES][words]
+    inst_range: np.ndarray   # uint32 [P]
+    inst: np.ndarray         # uint32 [I]
+    shape_range: np.ndarray  # uint32 [S]
+    shape_area: np.ndarray   # int32 [S]
+    shape_off: np.ndarray    # int8 [O][2]
+
+
+def _bits_of(mask, pitch, words):
+    """Boolean [X][Y] plane -> uint64 [words] bitboard (bit x*pitch + y)."""
+    out = np.zeros(words, np.uint64)
+    xs, ys = np.nonzero(mask)
+    for x, y in zip(xs.tolist(), ys.tolist()):
+        b = x * pitch + y
+        out[b >> 6] |= np.uint64(1) << np.uint64(b & 63)
+    return out
+
+
+def shape_offsets(shape_arr):
+    """_get_offsets (SPaRC_Gym.py:840-855) in cell units: the anchor is the first 1 of the
+    shape's first row that has one."""
+    s = np.array(shape_arr, dtype=np.int32)
+    xs, ys = np.where(s == 1)
+    if len(xs) == 0:
+        return []
+    ax = xs.min()
+    ay = ys[np.where(xs == ax)[0]].min()
+    return [(int(x - ax), int(y - ay)) for x, y in zip(xs, ys)]
+
+
+def pack_rules(puzzles, table: PuzzleTable) -> RulesTable:
+    """Processed puzzles -> the rule-audit table, on ``table``'s geometry.
+
+    Restates what `_validate_rules` reads from a puzzle (SPaRC_Gym.py:372-838) as bit-planes:
+    the symbol layers of `_collect_region_symbols` (456-481) only count at cell centres (the
+    only points with a region id), triangles only at x in 1..x_size-2 / y in 1..y_size-2 with
+    count > 0 (630-636), poly/ylop instances are the cells whose additional_info names a
+    polyshape key (714-734).  Like the reference (734), a pool with a shaped instance and no
+    'poly' layer raises KeyError('poly').
+    """
+    pitch, W = table.pitch, table.words
+    P = len(puzzles)
+    planes = np.zeros((P, RULE_PLANES, W), np.uint64)
+    inst_range = np.zeros(P, np.uint32)
+    inst, shapes, shape_ids = [], [], {}
+    for q, p in enumerate(puzzles):
+        X, Y = int(p["x_size"]), int(p["y_size"])
+        obs = p["obs_array"]
+        color = np.asarray(p["color_array"])[:X, :Y]
+        add = np.asarray(p["additional_info"])[:X, :Y]
+        xs, ys = np.meshgrid(np.arange(X), np.arange(Y), indexing="ij")
+        cells = (xs % 2 == 1) & (ys % 2 == 1)
+        layer = lambda k: (np.asarray(obs[k])[:X, :Y] == 1) if k in obs else np.zeros((X, Y), bool)  # noqa: E731
+        planes[q, RP_CELLS] = _bits_of(cells, pitch, W)
+        planes[q, RP_LATTICE] = _bits_of(np.ones((X, Y), bool), pitch, W)
+        planes[q, RP_GAPS] = _bits_of(layer("gaps"), pitch, W)
+        planes[q, RP_DOTS] = _bits_of(layer("dot"), pitch, W)
+        inner = (xs >= 1) & (xs <= X - 2) & (ys >= 1) & (ys <= Y - 2)
+        tri = layer("triangle") & inner & (add > 0)
+        cnt = np.clip(add, 0, 7)
+        planes[q, RP_TRI] = _bits_of(tri, pitch, W)
+        for k in range(3):
+            planes[q, RP_TRI0 + k] = _bits_of(tri & (((cnt >> k) & 1) == 1), pitch, W)
+        planes[q, RP_STAR] = _bits_of(layer("star") & cells, pitch, W)
+        planes[q, RP_SQUARE] = _bits_of(layer("square") & cells, pitch, W)
+        planes[q, RP_COLORED] = _bits_of((color != 0) & cells, pitch, W)
+        for c in range(1, 9):
+            planes[q, RP_COL1 + c - 1] = _bits_of((color == c) & cells, pitch, W)
+        mult = np.zeros((X, Y), np.int64)
+        for k in obs:
+            if k not in RULE_SKIP_LAYERS:
+                mult += layer(k)
+        mult = np.where(cells, mult, 0)
+        if mult.max(initial=0) > 7:
+            raise ValueError(f"puzzle {q}: more than 7 symbol layers on one cell")
+        for k in range(3):
+            planes[q, RP_M0 + k] = _bits_of(((mult >> k) & 1) == 1, pitch, W)
+        planes[q, RP_NOTFIRST] = _bits_of(ys != 0, pitch, W)
+        planes[q, RP_NOTLAST] = _bits_of(ys != Y - 1, pitch, W)
+        first = len(inst)
+        poly = p["polyshapes"]
+        if isinstance(poly, dict):
+            for x in range(X):                                        # _extract_poly_instances
+                for y in range(Y):
+                    val = add[x, y]
+                    if val == 0 or f"{val}" not in poly:
+                        continue
+                    name = f"{val}"
+                    ylop = not (np.asarray(obs["poly"])[x, y] == 1)   # KeyError('poly') as at 734
+                    if not cells[x, y]:
+                        continue                                      # region id -1 (687-690)
+                    arr = poly[name]
+                    offs = shape_offsets(arr)
+                    key = (tuple(offs), int(np.array(arr).sum()))
+                    if key not in shape_ids:
+                        shape_ids[key] = len(shapes)
+                        shapes.append(key)
+                    b = x * pitch + y
+                    inst.append(b | (int(ylop) << 10) | (((x - 1) // 2) << 11) | (((y - 1) // 2) << 14)
+                                | (shape_ids[key] << 17))
+        if len(inst) - first > 0xFFFF or first > 0xFFFF:
+            raise ValueError("too many poly/ylop instances for the rule table")
+        inst_range[q] = first | ((len(inst) - first) << 16)
+    offs, srange, sarea = [], [], []
+    for o, area in shapes:
+        srange.append(len(offs) | (len(o) << 16))
+        sarea.append(area)
+        offs.extend(o)
+    if len(offs) > 0xFFFF or len(shapes) >= 1 << 15:
+        raise ValueError("too many polyshapes for the rule table")
+    return RulesTable(planes, inst_range, np.asarray(inst, np.uint32), np.asarray(srange, np.uint32),
+                      np.asarray(sarea, np.int32), np.asarray(offs, np.int8).reshape(-1, 2))

@@ -19,6 +19,10 @@ Observations (``observation='new'``): ``visited`` and ``agent_location`` as int3
 static planes (gaps, target, symbols, color, additional_info) of every puzzle are in
 ``static_planes`` and ``static_keys`` (``static_planes[puzzle_index]`` gives an env's).
 ``observation='compact'`` returns only ``puzzle_index`` and the agent location.
+
+Rule audit (``rules=True``, or ``rule_audit()`` on demand): the reference's
+``info['rule_status']`` (SPaRC_Gym.py:941-950) evaluated by the k_rules kernel for every env,
+as ``info['rule_bits']`` [N] int16 with bit k = ``RULE_NAMES[k]`` passed.
 """
 from __future__ import annotations
 
@@ -27,7 +31,11 @@ import torch
 
 from .core import SparcCore
 from .env import load_puzzle_source
-from .puzzles import pack_table, process_puzzles
+from .puzzles import pack_rules, pack_table, process_puzzles
+
+RULE_NAMES = ("reached_target", "path_not_crossing", "no_gap_violations", "all_dots_collected",
+              "square_color_separation", "star_pairing_exact", "triangles_edge_count", "poly_ylop_area",
+              "all_rules_satisfied")   # _run_rule_validators order, SPaRC_Gym.py:908-936
 
 # reward code -> float64 value; code/100 in float64 is exactly the reference's 0.01/-0.01 double
 REWARD_SCALE = 100.0
@@ -36,7 +44,7 @@ REWARD_SCALE = 100.0
 class SPaRCVecEnv:
     def __init__(self, num_envs, puzzles=None, df_name="lkaesberg/SPaRC", df_split="all", df_set="test",
                  observation="new", traceback=False, max_steps=2000, autoreset="next_step", device=0,
-                 env_offset=0, pitch=None, words=None, processed=None, table=None):
+                 env_offset=0, pitch=None, words=None, processed=None, table=None, rules=False):
         if observation not in ("new", "compact"):
             raise ValueError("observation must be 'new' or 'compact' for the vector env")
         self.num_envs = int(num_envs)
@@ -63,6 +71,10 @@ class SPaRCVecEnv:
             self._agent = torch.empty_like(self._vis)
             self._build_static()
         self._cursor = np.arange(n, dtype=np.int64) % self.num_puzzles   # "__init__ loads" env i -> i mod P
+        self.rules = bool(rules)
+        self._rbits = None
+        if self.rules:
+            self._load_rules()
         self._np_random = None
         self._bound_stream = None
 
@@ -105,6 +117,28 @@ class SPaRCVecEnv:
         return {"visited": self._vis, "agent_location": self._agent, "puzzle_index": self._pidx,
                 "agent_xy": loc}
 
+    def _load_rules(self):
+        if self._rbits is None:
+            self.core.load_rules(pack_rules(self.puzzles, self.table))
+            self._rbits = torch.empty(self.num_envs, dtype=torch.int16, device=self.device)
+
+    def rule_audit(self, region=False, fit=False):
+        """The rule audit of every env's current state on the GPU (k_rules): dict with ``bits``
+        [N] int16 (bit k = RULE_NAMES[k] passed), optionally ``region`` [N, 64*words] uint8
+        (region id per cell bit, the reference's numbering; 255 elsewhere) and ``fit`` [N]
+        int64 (bit r: region r passed the poly/ylop area check and exact fit)."""
+        self._stream()
+        self._load_rules()
+        n = self.num_envs
+        out = {"bits": self._rbits}
+        if region:
+            out["region"] = torch.empty((n, 64 * self.table.words), dtype=torch.uint8, device=self.device)
+        if fit:
+            out["fit"] = torch.empty(n, dtype=torch.int64, device=self.device)
+        self.core.rules_device(self._rbits.data_ptr(), out["region"].data_ptr() if region else None,
+                               out["fit"].data_ptr() if fit else None)
+        return out
+
     @property
     def np_random(self):
         if self._np_random is None:
@@ -135,6 +169,8 @@ class SPaRCVecEnv:
         self._cursor = q.copy()
         flags = self.core.reset_host(q.astype(np.uint32))
         info = {"legal_mask": torch.from_numpy(((flags >> 2) & 0xF).astype(np.uint8)).to(self.device)}
+        if self.rules:
+            info["rule_bits"] = self.rule_audit()["bits"]
         return self._obs(), info
 
     def step(self, actions):
@@ -153,6 +189,8 @@ class SPaRCVecEnv:
         terminated = (f & 1).bool()
         truncated = (f & 2).bool()
         info = {"legal_mask": (f >> 2) & 0xF, "autoreset": (f & 64).bool(), "reward_code": self._rew}
+        if self.rules:
+            info["rule_bits"] = self.rule_audit()["bits"]
         return self._obs(), reward, terminated, truncated, info
 
     def rollout(self, T, actions=None, seed=0, t0=0, stats=None, record=True, out=None):

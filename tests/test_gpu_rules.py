@@ -1,0 +1,117 @@
+"""GPU parity of the rule audit (k_rules through the C ABI): the pass bits, region map and
+exact-fit results against the reference's rule_status golden vectors, SPaRC_Gym's full
+info['rule_status'] dict against the same vectors, and the bits at the benchmark's 65,536 envs
+against the oracle (oracle/rules_ref.py) on a sample of envs."""
+import numpy as np
+import pytest
+
+from golden_io import load
+from oracle import rules_ref
+from rules_io import RULE_POOLS, ref_puzzle
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def _fit_mask(status):
+    m = 0
+    for d in status["poly_ylop_area"]["detail"].get("region_details", []):
+        if d["ok"]:
+            m |= 1 << int(d["region"])
+    return m
+
+
+def _region_bits(refp, s, pitch, words):
+    _, rm = rules_ref.RuleAudit(refp, s["path"], s["agent"]).compute_regions()
+    out = np.full(64 * words, 255, np.uint8)
+    for x in range(rm.shape[0]):
+        for y in range(rm.shape[1]):
+            if rm[x, y] >= 0:
+                out[x * pitch + y] = rm[x, y]
+    return out
+
+
+@pytest.mark.parametrize("pool", RULE_POOLS)
+def test_vec_rules_match_reference(on_gpu, pool):
+    from sparc_gym_amd import SPaRCVecEnv
+    g = load(pool)
+    eps = g["episodes"]
+    n, T = len(eps), max(len(e["actions"]) for e in eps)
+    vec = SPaRCVecEnv(n, puzzles=g["records"], traceback=g["traceback"], max_steps=2000, autoreset="none",
+                      rules=True)
+    refp = [ref_puzzle(p) for p in g["processed"]]
+    pitch, words = vec.table.pitch, vec.table.words
+    _, info = vec.reset(options={"puzzle_index": [e["puzzle_index"] for e in eps]})
+    acts = np.full((T, n), 255, np.int64)
+    for i, e in enumerate(eps):
+        acts[:len(e["actions"]), i] = e["actions"]
+    for t in range(-1, T):
+        if t >= 0:
+            vec.step(torch.from_numpy(acts[t]).cuda())
+        r = vec.rule_audit(region=True, fit=True)
+        bits = r["bits"].cpu().numpy().astype(np.uint16)
+        region, fit = r["region"].cpu().numpy(), r["fit"].cpu().numpy().astype(np.uint64)
+        for i, e in enumerate(eps):
+            if t >= len(e["steps"]):
+                continue
+            s = e["reset"] if t < 0 else e["steps"][t]
+            assert int(bits[i]) == rules_ref.rule_bits(s["rule_status"]), (pool, i, t)
+            assert int(fit[i]) == _fit_mask(s["rule_status"]), (pool, i, t)
+            assert np.array_equal(region[i], _region_bits(refp[e["puzzle_index"]], s, pitch, words)), (pool, i, t)
+
+
+@pytest.mark.parametrize("pool", RULE_POOLS)
+def test_single_env_rule_status_matches_reference(on_gpu, pool):
+    """SPaRC_Gym's info['rule_status'] equals the reference's, the whole nested dict."""
+    from sparc_gym_amd import SPaRC_Gym
+    g = load(pool)
+    env = SPaRC_Gym(puzzles=g["records"], traceback=g["traceback"], max_steps=2000)
+    ids = [r["id"] for r in g["records"]]
+    for e, ep in enumerate(g["episodes"][:12]):
+        _, info = env.reset(options={"puzzle_id": ids[ep["puzzle_index"]]})
+        assert rules_ref.normalize(info["rule_status"]) == ep["reset"]["rule_status"], (pool, e)
+        for t, (a, s) in enumerate(zip(ep["actions"], ep["steps"])):
+            _, _, _, _, info = env.step(a)
+            assert rules_ref.normalize(info["rule_status"]) == s["rule_status"], (pool, e, t)
+            assert info["rule_status"] is env.rule_status
+
+
+def _state_points(vis_words, pitch, X, Y):
+    v = sum(int(w) << (64 * k) for k, w in enumerate(vis_words))
+    return [[x, y] for x in range(X) for y in range(Y) if (v >> (x * pitch + y)) & 1]
+
+
+# random symbol soups only up to 11x11: on 13x13 / 15x15 boards they can hold regions with many
+# ylops, whose exact-fit search (anchors^ylops, as in the reference) is effectively unbounded
+@pytest.mark.parametrize("sizes,full,n", [(((3, 3),), True, 65536), (((2, 2), (3, 3), (4, 4), (5, 5)), True, 8192),
+                                          (((7, 7), (6, 6)), False, 4096)])
+def test_rules_at_scale_vs_oracle(on_gpu, sizes, full, n):
+    """After a device rollout of random actions, k_rules bits equal the oracle's on a sample."""
+    from sparc_gym_amd import SPaRCVecEnv, synthetic
+    from sparc_gym_amd.puzzles import process_puzzles
+    recs = synthetic.make_rule_puzzles(256, seed=8, sizes=sizes, break_prob=0.3)
+    if full:
+        recs += synthetic.make_puzzles(256, seed=7, sizes=sizes, full_properties=True)
+    proc = process_puzzles(recs)
+    vec = SPaRCVecEnv(n, processed=proc, traceback=True, autoreset="next_step", observation="compact",
+                      rules=True)
+    gid = np.arange(n, dtype=np.uint64)
+    vec.reset(options={"puzzle_index": (gid * 2654435761 % len(proc)).astype(np.int64)})
+    refp = [dict(p) for p in proc]
+    rng = np.random.default_rng(0)
+    checked = 0
+    for T in (0, 7, 40):
+        if T:
+            vec.rollout(T, None, seed=T, record=False)
+        bits = vec.rule_audit()["bits"].cpu().numpy().astype(np.uint16)
+        st = vec.state()
+        for i in rng.choice(n, size=400, replace=False):
+            q = int(st["puzzle"][i])
+            p = refp[q]
+            path = _state_points(st["visited"][:, i], vec.table.pitch, p["x_size"], p["y_size"])
+            want = rules_ref.rule_bits(rules_ref.audit(p, path, (int(st["x"][i]), int(st["y"][i]))))
+            assert int(bits[i]) == want, (T, i, q)
+            checked += 1
+    vec.core.sync()
+    assert checked == 1200
