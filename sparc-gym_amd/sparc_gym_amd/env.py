@@ -21,6 +21,7 @@ Differences (documented in DESIGN.md):
 from __future__ import annotations
 
 import json
+import os
 from collections import OrderedDict
 
 import numpy as np
@@ -50,10 +51,35 @@ def action_code(action):
 
 
 def load_puzzle_source(puzzles, df_name, df_split, df_set):
-    if puzzles is not None:
-        return puzzles
-    from datasets import load_dataset   # SPaRC_Gym.py:77-78 (network on first use)
-    return load_dataset(df_name, df_split, split=df_set).to_pandas()
+    """The puzzle DataFrame of SPaRC_Gym.__init__ (77-78).
+
+    ``puzzles`` may be a DataFrame, a list of records, or a local path: a ``.parquet`` file, a
+    directory of parquet files (a local export of the ``lkaesberg/SPaRC`` split, read in sorted
+    file order), or a ``.json`` / ``.jsonl`` file of records.  Without ``puzzles`` the hub
+    dataset is loaded as the reference does (needs the network, or a local HF cache)."""
+    if puzzles is None:
+        from datasets import load_dataset   # SPaRC_Gym.py:77-78
+        return load_dataset(df_name, df_split, split=df_set).to_pandas()
+    if isinstance(puzzles, (str, os.PathLike)):
+        return load_local(os.fspath(puzzles))
+    return puzzles
+
+
+def load_local(path):
+    """DataFrame of SPaRC records from a local parquet file / directory or json(l) file."""
+    import pandas as pd
+    if os.path.isdir(path):
+        files = sorted(os.path.join(path, f) for f in os.listdir(path) if f.endswith(".parquet"))
+        if not files:
+            raise ValueError(f"no .parquet files in {path}")
+        return pd.concat([pd.read_parquet(f) for f in files], ignore_index=True)
+    if path.endswith(".parquet"):
+        return pd.read_parquet(path)
+    if path.endswith(".jsonl"):
+        return pd.read_json(path, lines=True, dtype=False)
+    if path.endswith(".json"):
+        return pd.read_json(path, dtype=False)
+    raise ValueError(f"unsupported puzzle file {path!r} (.parquet, a parquet directory, .json or .jsonl)")
 
 
 class SPaRC_Gym(Env):
