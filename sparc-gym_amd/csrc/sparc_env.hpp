@@ -70,6 +70,7 @@ struct Params {
     int32_t autoreset;
     uint64_t env_offset;
     int32_t* __restrict__ err;
+    uint32_t nbr_pos;   // W = 1: window bit of each direction's neighbour, one byte per direction
 };
 
 // Static puzzle rows, from global memory or from an LDS copy (same layout).  info.w holds the
@@ -82,7 +83,7 @@ struct PuzzleSrc {
     const uint64_t* open;
     const uint64_t* init;
     const uint4* row1;     // W = 1: {start_bit | target_bit<<8 | flags<<16, trie_base,
-                           //         trie_cnt | legal0<<16, 0}
+                           //         trie_max | legal0<<16, 0}; init: free board at reset
     __device__ __forceinline__ uint4 get_row1(uint32_t q) const { return row1[q]; }
     __device__ __forceinline__ uint4 get_info(uint32_t q) const { return info[q]; }
     __device__ __forceinline__ uint4 get_root(uint32_t q) const { return root[q]; }
@@ -354,49 +355,58 @@ struct Env {
 };
 
 // ---------------------------------------------------------------------------------------------
-// Direction stacks of the W = 1 path (2 bits of information per move, <= 62 moves on a 64-bit
-// board).  In HBM both are stored as two u64 words [2][N] (move k at bits 2(k%32) of word k/32).
+// Direction stacks of the W = 1 path (2 bits of information per move, <= 63 moves on a 64-bit
+// board).  Registers / LDS hold the REVERSED moves (move k ^ 2 = the direction from path[k+1]
+// back to path[k]), which is what the traceback rule and the pop need; in HBM both are stored
+// as the moves themselves, two u64 words [2][N] (move k at bits 2(k%32) of word k/32), only
+// the path's len-1 moves set.  Writes are unconditional: a step writes slot len-1, which is
+// the new top after a forward move and lies above the top otherwise.
+constexpr uint64_t kRev2 = 0xAAAAAAAAAAAAAAAAull;   // XOR: move <-> reversed move, every field
+__device__ __forceinline__ uint64_t low_moves(uint32_t moves, uint32_t word) {
+    // mask of the fields of `moves` moves that live in word `word` (0: moves 0-31)
+    const uint32_t m = word ? (moves > 32u ? moves - 32u : 0u) : (moves < 32u ? moves : 32u);
+    return m >= 32u ? ~0ull : ((1ull << (2u * m)) - 1ull);
+}
+
 struct RegStack {            // k_step / k_reset: two u64 registers
     uint64_t lo = 0, hi = 0;
     __device__ __forceinline__ void clear() { lo = hi = 0; }
     __device__ __forceinline__ uint32_t read(uint32_t k) const {
         return (uint32_t)((k < 32 ? lo : hi) >> ((k & 31u) * 2u)) & 3u;
     }
-    __device__ __forceinline__ void write_if(bool en, uint32_t k, uint32_t d) {
+    __device__ __forceinline__ void write(uint32_t k, uint32_t d) {
         const uint32_t sh = (k & 31u) * 2u;
         const bool hiw = k >= 32;
         const uint64_t w = hiw ? hi : lo;
-        const uint64_t upd = (w & ~(3ull << sh)) | ((uint64_t)d << sh);
-        lo = (en & !hiw) ? upd : lo;
-        hi = (en & hiw) ? upd : hi;
+        const uint64_t upd = (w & ~(3ull << sh)) | ((uint64_t)(d & 3u) << sh);
+        lo = hiw ? lo : upd;
+        hi = hiw ? upd : hi;
     }
     __device__ __forceinline__ void load(const uint64_t* d, size_t n, uint32_t i, uint32_t) {
-        lo = d[i];
-        hi = d[n + i];
+        lo = d[i] ^ kRev2;
+        hi = d[n + i] ^ kRev2;
     }
-    __device__ __forceinline__ void store(uint64_t* d, size_t n, uint32_t i, uint32_t) const {
-        d[i] = lo;
-        d[n + i] = hi;
+    __device__ __forceinline__ void store(uint64_t* d, size_t n, uint32_t i, uint32_t moves) const {
+        d[i] = (lo ^ kRev2) & low_moves(moves, 0);
+        d[n + i] = (hi ^ kRev2) & low_moves(moves, 1);
     }
 };
 
 template <uint32_t S>         // k_rollout: one byte per move in this lane's column of a per-wave
-struct LdsStack {            // [64 moves][S lanes] LDS array; slot 63 is a write sink
+struct LdsStack {            // [64 moves][S lanes] LDS array
     uint8_t* col;
     __device__ __forceinline__ void clear() {}
     __device__ __forceinline__ uint32_t read(uint32_t k) const { return col[k * S]; }
-    __device__ __forceinline__ void write_if(bool en, uint32_t k, uint32_t d) {
-        col[(en ? k : 63u) * S] = (uint8_t)d;
-    }
+    __device__ __forceinline__ void write(uint32_t k, uint32_t d) { col[k * S] = (uint8_t)d; }
     __device__ __forceinline__ void load(const uint64_t* d, size_t n, uint32_t i, uint32_t moves) {
-        const uint64_t lo = d[i], hi = d[n + i];
+        const uint64_t lo = d[i] ^ kRev2, hi = d[n + i] ^ kRev2;
         for (uint32_t k = 0; k < moves; ++k)
             col[k * S] = (uint8_t)(((k < 32 ? lo : hi) >> ((k & 31u) * 2u)) & 3u);
     }
     __device__ __forceinline__ void store(uint64_t* d, size_t n, uint32_t i, uint32_t moves) const {
         uint64_t lo = 0, hi = 0;
         for (uint32_t k = 0; k < moves; ++k) {
-            const uint64_t v = (uint64_t)col[k * S] << ((k & 31u) * 2u);
+            const uint64_t v = (uint64_t)((col[k * S] ^ 2u) & 3u) << ((k & 31u) * 2u);
             lo |= k < 32 ? v : 0ull;
             hi |= k < 32 ? 0ull : v;
         }
@@ -406,24 +416,29 @@ struct LdsStack {            // [64 moves][S lanes] LDS array; slot 63 is a writ
 };
 
 // ---------------------------------------------------------------------------------------------
-// W = 1 specialisation: lattices that fit a 64-bit board PADDED by one blocked column
-// (pitch > y_size) and one blocked row (x_size + 1 rows), i.e. (x_size + 1) * pitch <= 64
-// (every 7x7 and 5x5 pool; the host packer picks this geometry).  The agent is the bit index
-// b = x*pitch + y; `blk` = visited | not-open is the only bitboard in registers, and the four
-// neighbour tests of _get_legal_actions are one 32-bit window of blk starting at b - pitch
-// (bits 0: left, pitch-1: up, pitch+1: down, 2*pitch: right), with no bounds compares
-// (out-of-lattice neighbours are padding = blocked; below bit 0 reads as blocked).  The step is
-// branch-free except for the autoreset and the trie-record load, and is ordered so that the
-// record gathered at one step's transition is first read at the next step's transition.
+// W = 1 specialisation: lattices that fit a 64-bit board PADDED by one column (pitch > y_size)
+// and one row, (x_size + 1) * pitch <= 64 (every 7x7 and 5x5 pool; the host packer picks this
+// geometry).  The agent is the bit index e = x*pitch + y.  The only bitboard in registers is
+// the FREE board `fr` (in the lattice, not a gap, unvisited) stored one row up: bit e + pitch
+// is point e.  So the four neighbour tests of _get_legal_actions are one 64-bit shift,
+//     w = (uint32_t)(fr >> e):  bit 0 left (x-1), pitch-1 up (y-1), pitch+1 down (y+1),
+//                               2*pitch right (x+1)
+// and every out-of-lattice neighbour reads 0: below row 0 is the empty bottom row, beyond
+// y_size-1 the empty padding column, beyond the last row either the empty top row or bits
+// shifted out of the word.  No bounds compares, no rotate.  The step is branch-free except
+// for the autoreset and is ordered so that the trie record gathered at the end of one step is
+// first read in the next step's trie phase.
 template <bool TB, class Stack>
 struct Env<1, TB, Stack> {
-    uint64_t blk;        // blocked: visited | ~open (padding and gaps included)
-    Stack stk;           // moves of self.path (traceback only)
-    uint32_t b, len, off, node, node_term, outcome, pending, step, pid, legal, last;
-    uint32_t tgt, pflags, trie_base, trie_cnt;
-    uint32_t prev_next = 0;   // traceback: move before the last one, read one step ahead
+    uint64_t fr;         // free board, one row up (bit e + pitch = point e)
+    Stack stk;           // reversed moves of self.path (traceback only)
+    uint32_t e, len, off, node, node_term, outcome, pending, pid, legal, rl;
+    int32_t step;
+    uint32_t tgt, pflags, trie_base, trie_max;
+    uint32_t bk;         // traceback rule bias: (len + bk) >> 31 = len >= 3 or (len == 2, open start)
+    uint32_t w = 0;      // window of fr at e (see above), valid between steps
+    uint32_t pnr = 0;    // traceback: reversed move before the last one, read one step ahead
     uint32_t solved = 0, was_reset = 0;   // this step: a +1 outcome / an autoreset (for stats)
-    uint32_t bad = 0;         // sticky: a trie index was out of range (reported at store)
     uint4 rec;
 
     // all arms are computed unconditionally and merged with masks: a C++ ?: whose arms are
@@ -433,62 +448,57 @@ struct Env<1, TB, Stack> {
         return (a & m) | (b & ~m);
     }
 
-    __device__ __forceinline__ uint32_t legal_mask(uint32_t P) const {
-        // 32-bit window whose bit j is blocked(b - P + j): a 64-bit rotate, because the top
-        // rows of the board (x >= x_size, all padding) are blocked and so read correctly as the
-        // out-of-lattice cells below row 0 ((x_size + 1) * pitch <= 64)
-        const uint32_t w = ~(uint32_t)__builtin_rotateright64(blk, (b - P) & 63u);   // free bits
-        // up (bit P-1) and down (bit P+1) land on bits 1 and 3 with one shift and mask
-        uint32_t m = (((w >> (P - 1)) & 5u) << 1) | ((w >> (2 * P)) & 1u) | ((w << 2) & 4u);
-        if constexpr (TB) {
-            // path[-2] is the reverse of the last move; it is open unless it is a closed start
-            const uint32_t back = (uint32_t)(len >= 3) | ((uint32_t)(len == 2) & ((~pflags >> 2) & 1u));
-            m |= back << (last ^ 2u);
-        }
+    // _get_legal_actions (1024-1051): bit d = direction d is legal; sets the window w
+    __device__ __forceinline__ uint32_t legal_mask(uint32_t P) {
+        w = (uint32_t)(fr >> (e & 63u));
+        const uint32_t ud = __builtin_amdgcn_ubfe(w, P - 1u, 3u);   // up, self, down
+        uint32_t m = ((ud & 5u) << 1) | __builtin_amdgcn_ubfe(w, 2u * P, 1u) | ((w << 2) & 4u);
+        // traceback: path[-2] (the reverse of the last move) is visited but legal
+        if constexpr (TB) m |= ((len + bk) >> 31) << rl;
         return m;
     }
 
+    // row: {start | target<<8 | flags<<16, trie_base, trie_max | legal0<<16, 0}; flags bit0
+    // solutions, bit1 root valid, bit2 start closed, bit3 root terminal
     template <class Src>
-    __device__ __forceinline__ uint32_t load_puzzle(const Src& src, uint32_t q, uint32_t) {
+    __device__ __forceinline__ uint32_t load_puzzle(const Src& src, uint32_t q) {
         const uint4 r = src.get_row1(q);
         tgt = (r.x >> 8) & 0xFFu;
         pflags = r.x >> 16;
         trie_base = r.y;
-        trie_cnt = r.z & 0xFFFFu;
-        legal = r.z >> 16;
-        return r.x & 0xFFu;   // start bit
+        trie_max = r.z & 0xFFFFu;
+        bk = 0x7FFFFFFDu + ((~pflags >> 2) & 1u);
+        return r.x & 0xFFu;   // start
     }
 
-    // The current node's record, loaded unconditionally (L2-resident table): one destination
-    // write per step keeps the compiler from merging / copying an in-flight load, so its first
-    // wait sits at the next step's trie phase.  node < trie_cnt holds on validated tables; a
-    // violation is recorded in `bad` instead of reading out of bounds.
+    // the current node's record, loaded unconditionally (L2-resident table); node <= trie_max
+    // holds on validated tables, the clamp keeps a broken state from reading out of bounds
     __device__ __forceinline__ void load_rec(const Params& p) {
-        const bool oob = node >= trie_cnt;
-        bad |= (oob & (bool)(pflags & 2u)) ? 1u : 0u;
-        rec = p.tab.trie[trie_base + (oob ? 0u : node)];
+        rec = p.tab.trie[trie_base + (node < trie_max ? node : trie_max)];
     }
 
-    // _load_puzzle (SPaRC_Gym.py:166-187) with fresh planes: precomputed board and legal mask;
-    // the root record arrives through the next load_rec (node = 0)
+    // _load_puzzle (SPaRC_Gym.py:166-187) with fresh planes; step0 = -1 inside a rollout (the
+    // same step's counter increment brings it to 0).  Inside a rollout the step that resets
+    // recomputes pending, outcome and legal itself, and rl is unused until the first move.
     template <class Src>
-    __device__ __forceinline__ void reset_rows(const Src& src, uint32_t P, uint32_t q) {
+    __device__ __forceinline__ void reset_rows(const Src& src, uint32_t q) {
         pid = q;
-        b = load_puzzle(src, q, P);
-        blk = src.get_init(q);
-        len = 1;
-        node = 0;
-        off = (pflags & 2u) ? 0u : 1u;
+        e = load_puzzle(src, q);
+        fr = src.get_init(q);
+        off = ((pflags >> 1) & 1u) ^ 1u;
         node_term = (pflags >> 3) & 1u;   // the root is itself a solution ([start])
-        outcome = 0;
-        pending = 0;
-        step = 0;
-        last = 0;
-        stk.clear();
     }
     template <class Src>
     __device__ __forceinline__ void reset(const Params& p, const Src& src, uint32_t q) {
-        reset_rows(src, p.pitch, q);
+        reset_rows(src, q);
+        len = 1;
+        node = 0;
+        step = 0;
+        outcome = 0;
+        pending = 0;
+        rl = 0;
+        stk.clear();
+        legal = legal_mask(p.pitch);
         load_rec(p);
     }
 
@@ -496,47 +506,58 @@ struct Env<1, TB, Stack> {
     __device__ __forceinline__ int advance(const Params& p, const Src& src, uint32_t a, uint32_t& flags) {
         const uint32_t P = p.pitch;
         // gymnasium next-step autoreset (reset(), SPaRC_Gym.py:1087): the reset lanes run the
-        // same phases below as a no-move step whose outputs are overridden
-        const bool rst = (p.autoreset == 1) & (pending != 0);
-        if (rst) reset_rows(src, P, pid + 1 == p.tab.num_puzzles ? 0u : pid + 1);
-        // ---- phase 1: move, visited, path, legality, flags (no trie record needed)
-        step += (uint32_t)(!rst & (step < 0x7FFFFFFFu));                          // 1132
-        const bool trunc0 = (int32_t)step >= p.max_steps;                          // 1134
-        const uint32_t ad = a & 3u;
-        // `action in legal` (1137): bit a of the legal mask; actions >= 4 read bit 4 (always 0)
-        const uint32_t lg = rst ? 0u : legal;
-        const bool moved = (lg >> (a < 4u ? a : 4u)) & 1u;
-        // neighbour offset: right +P, up -1, left -P, down +1, as signed bytes of one constant
-        const uint32_t deltas = (P & 0xFFu) | (0xFFu << 8) | (((0u - P) & 0xFFu) << 16) | (1u << 24);
-        const uint32_t nb = b + (uint32_t)__builtin_amdgcn_sbfe((int)deltas, ad * 8u, 8u);
-        // the only legal move onto a blocked (visited) cell is the traceback pop (1141-1166)
-        const bool pop = TB & moved & (bool)((blk >> (nb & 63u)) & 1ull);
-        const bool fwd = moved & !pop;                                             // 1167-1188
-        // visited: forward sets the new node, a pop clears the node it leaves
-        const uint32_t tog = pick(fwd, nb, b);
-        blk ^= (uint64_t)moved << (tog & 63u);   // (an illegal move's nb may be out of range)
+        // same phases below as a no-move step (legal = 0) whose outputs are overridden
+#ifdef SPARC_DIAG_NO_RESET
+        const uint32_t live = ~0u;
+#else
+        const uint32_t live = (pending & (uint32_t)(p.autoreset == 1)) - 1u;   // 0 on reset lanes
+#endif
+        if (live == 0u) reset_rows(src, pid + 1 == p.tab.num_puzzles ? 0u : pid + 1);
+        // the rest of the reset as masks (no exec-masked merge block): len 1, root node, and
+        // step -1, which this step's increment brings to 0
+        len = (len & live) | (1u & ~live);
+        node &= live;
+        step = (int32_t)((uint32_t)step | ~live);
+        // ---- phase 1: move, free board, path, legality, flags (no trie record needed)
+        step = __builtin_elementwise_add_sat(step, 1);                              // 1132
+        const bool trunc0 = step >= p.max_steps;                                    // 1134
+        // `action in legal` (1137): bit a of the legal mask; actions >= 4 read bit 4 (0); a
+        // reset step does not move
+        const uint32_t moved = (legal >> (a < 4u ? a : 4u)) & live & 1u;
+        // neighbour's bit in the window: right 2P, up P-1, left 0, down P+1 (bytes of one
+        // constant; the bfe offset keeps 5 bits, so a<<3 selects byte a&3)
+        const uint32_t pos = __builtin_amdgcn_ubfe(p.nbr_pos, a << 3, 8u);
+        // the only legal move onto a non-free point is the traceback pop (1141-1166)
+        const uint32_t pop = TB ? moved & ~__builtin_amdgcn_ubfe(w, pos, 1u) : 0u;
+        const uint32_t fwd = moved ^ pop;                                            // 1167-1188
+        // free board: a forward move takes the target (bit e + pos), a pop frees the point it
+        // leaves (bit e + P)
+        const uint32_t tog = e + (fwd ? pos : P);
+        fr ^= (uint64_t)moved << (tog & 63u);
         if constexpr (TB) {
-            stk.write_if(fwd, len - 1u, ad);    // push `a` at move index len-1
-            last = pick(fwd, ad, pick(pop, prev_next, last));
+            const uint32_t ar = a ^ 2u;
+            stk.write(len - 1u, ar);                 // the new top if fwd, above the top otherwise
+            rl = fwd ? ar : (pop ? pnr : rl);
         }
-        len = len + (uint32_t)fwd - (uint32_t)pop;
-        b = pick(moved, nb, b);
+        len = len + fwd - pop;
+        e = moved ? e + pos - P : e;
         legal = legal_mask(P);
-        const bool term = (b == tgt) & !rst;                                       // 1192
-        const bool trunc = (trunc0 | (legal == 0)) & !term & !rst;                 // 1195-1199
+        const bool term = (e == tgt) & (live != 0u);                                 // 1192
+        const bool trunc = (trunc0 | (legal == 0)) & !term & (live != 0u);          // 1195-1199
         const bool done = term | trunc;
-        flags = (legal << 2) | pick(rst, 64u, (uint32_t)term | ((uint32_t)trunc << 1));
+        flags = (legal << 2) | (live ? (uint32_t)term | ((uint32_t)trunc << 1) : 64u);
         pending = (uint32_t)done;
-        if constexpr (TB) prev_next = stk.read(len >= 3 ? len - 3u : 0u);   // for the next step's pop
+        if constexpr (TB) pnr = stk.read(__builtin_elementwise_sub_sat(len, 3u));   // next step's pop
         __builtin_amdgcn_sched_barrier(0);
         // ---- phase 2: solution trie (first read of the record loaded at the previous step)
         const bool on = off == 0;
-        const uint32_t c = (uint32_t)((((uint64_t)rec.y << 32) | rec.x) >> (ad * 16u)) & 0xFFFFu;
+        const uint32_t c = (uint32_t)((((uint64_t)rec.y << 32) | rec.x) >> ((a << 4) & 63u)) & 0xFFFFu;
         const bool down = fwd & on & (c != kNone);
         const bool up = pop & on;
-        node_term = pick(down, rec_child_term(rec, ad), pick(up, rec_parent_term(rec), node_term));
+        node_term = pick(down, __builtin_amdgcn_ubfe(rec.z, 17u + a, 1u),
+                         pick(up, rec_parent_term(rec), node_term));
         node = pick(down, c, pick(up, rec_parent(rec), node));
-        off = pick(on, (uint32_t)(fwd & (c == kNone)), off + (uint32_t)fwd - (uint32_t)pop);
+        off = pick(on, (uint32_t)(fwd & (c == kNone)), off + fwd - pop);
 #ifndef SPARC_DIAG_NO_TRIE_LOAD
         load_rec(p);
 #endif
@@ -545,10 +566,10 @@ struct Env<1, TB, Stack> {
         // (0 if the puzzle has no solutions); an autoreset step returns 0
         const bool match = (off == 0) & (node_term != 0);
         const int c_done = match ? 100 : (outcome != 1 ? -100 : 0);
-        const int c_move = (moved & (bool)(pflags & 1u)) ? (off == 0 ? 1 : -1) : 0;
-        outcome = pick(done, pick(match | (outcome == 1), 1u, 2u), 0u);
+        const int c_move = (moved & pflags & 1u) ? (off == 0 ? 1 : -1) : 0;
+        outcome = done ? ((match | (outcome == 1)) ? 1u : 2u) : 0u;
         solved = (uint32_t)(done & match);
-        was_reset = (uint32_t)rst;
+        was_reset = (uint32_t)(live == 0u);
         return done ? c_done : c_move;
     }
 
@@ -558,25 +579,24 @@ struct Env<1, TB, Stack> {
         const uint32_t P = p.pitch;
         const uint64_t vis = s.vis[i];
         const uint32_t ps = s.pos[i], ax = s.aux[i];
-        b = (ps & 0xFFu) * P + ((ps >> 8) & 0xFFu);
+        e = (ps & 0xFFu) * P + ((ps >> 8) & 0xFFu);
         len = (ps >> 16) & 0xFFu;
         off = ps >> 24;
         node = ax & 0xFFFFu;
         outcome = (ax >> 16) & 3u;
         pending = (ax >> 18) & 1u;
         node_term = (ax >> 19) & 1u;
-        step = s.step[i];
+        step = (int32_t)s.step[i];
         pid = s.pid[i];
-        bad = 0;
-        load_puzzle(src, pid, P);
-        blk = vis | ~p.tab.open[pid];
+        load_puzzle(src, pid);
+        fr = (p.tab.open[pid] & ~vis) << P;
         load_rec(p);
         if constexpr (TB) {
             stk.load(s.dirs, p.n, i, len >= 1 ? len - 1 : 0u);
-            last = len >= 2 ? stk.read(len - 2) : 0u;
-            prev_next = stk.read(len >= 3 ? len - 3u : 0u);
+            rl = len >= 2 ? stk.read(len - 2) : 0u;
+            pnr = stk.read(__builtin_elementwise_sub_sat(len, 3u));
         } else {
-            last = 0;
+            rl = 0;
         }
         legal = legal_mask(P);
     }
@@ -586,14 +606,15 @@ struct Env<1, TB, Stack> {
         const State& s = p.st;
         const uint32_t P = p.pitch;
         const uint32_t sb = src.get_row1(pid).x & 0xFFu;
-        s.vis[i] = blk & (p.tab.open[pid] | (1ull << sb));     // the start is always visited
+        // visited = in the puzzle and not free, plus the start (always on the path, even when
+        // it is a gap)
+        s.vis[i] = ((~fr) >> P & p.tab.open[pid]) | (1ull << sb);
         if constexpr (TB) stk.store(s.dirs, p.n, i, len >= 1 ? len - 1 : 0u);
-        const uint32_t x = b / P, y = b - x * P;
+        const uint32_t x = e / P, y = e - x * P;
         s.pos[i] = x | (y << 8) | (len << 16) | (off << 24);
         s.aux[i] = node | (outcome << 16) | (pending << 18) | (node_term << 19);
-        s.step[i] = step;
+        s.step[i] = (uint32_t)step;
         s.pid[i] = pid;
-        if (bad) atomicOr(p.err, (int)kErrTrie);
     }
 };
 

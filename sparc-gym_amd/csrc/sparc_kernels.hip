@@ -184,18 +184,26 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
                     const int k = g + j;
                     uint32_t f;
                     const int code = e.advance(p, src, av[j], f);
+#ifndef SPARC_DIAG_NO_OUT_LDS
                     tr[k * EPW + lane] = (uint8_t)code;
                     tf[k * EPW + lane] = (uint8_t)f;
+#endif
+#ifdef SPARC_DIAG_NO_STATS
+                    if constexpr (false) {
+#else
                     if constexpr (W == 1) {   // per-step flags the W = 1 step already has
+#endif
                         acc.x += code;
                         acc.y += (int)e.pending;
                         acc.z += (int)e.solved;
                         acc.w += (int)e.was_reset;
                     } else {
+#ifndef SPARC_DIAG_NO_STATS
                         acc.x += code;
                         acc.y += (f & 3u) ? 1 : 0;
                         acc.z += ((f & 3u) && code == 100) ? 1 : 0;
                         acc.w += (f & 64u) ? 1 : 0;
+#endif
                     }
                 }
             }
@@ -339,6 +347,8 @@ Params make_params(const Ctx* c) {
     p.autoreset = c->cfg.autoreset;
     p.env_offset = (uint64_t)c->cfg.env_offset;
     p.err = c->err;
+    const uint32_t P = p.pitch;
+    p.nbr_pos = (2u * P) | ((P - 1u) << 8) | (0u << 16) | ((P + 1u) << 24);
     return p;
 }
 
@@ -540,8 +550,8 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
     }
     HIPCHK(c, hipMemcpy(c->t_root, roots.data(), sizeof(uint4) * P, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->t_open, t->open, sizeof(uint64_t) * P * W, hipMemcpyHostToDevice));
-    // device copy of info: w3 = trie node count | legal mask of the reset state << 16, and the
-    // reset board (~open | start) of the padded W = 1 layout
+    // device copy of info: w3 = trie node count | legal mask of the reset state << 16, and for
+    // the padded W = 1 layout the compact rows and the free board at reset
     std::vector<uint4> dinfo(P);
     std::vector<uint64_t> init(P, 0);
     std::vector<uint4> row1(P, make_uint4(0u, 0u, 0u, 0u));
@@ -564,9 +574,11 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
                               (inf[3] & 0xFFFFu) | (legal0 << 16));
         if (W == 1) {
             const uint32_t tx = inf[1] & 0xFF, ty = (inf[1] >> 8) & 0xFF;
-            init[q] = ~t->open[q] | (1ull << (sx * pitch + sy));
+            // free board at reset, one row up (Env<1>): open points except the start
+            init[q] = (t->open[q] & ~(1ull << (sx * pitch + sy))) << pitch;
+            const uint32_t cnt = inf[3] & 0xFFFFu;
             row1[q] = make_uint4((sx * pitch + sy) | ((tx * pitch + ty) << 8) | (dinfo[q].y & 0xFFFF0000u),
-                                 inf[2], (inf[3] & 0xFFFFu) | (legal0 << 16), 0u);
+                                 inf[2], (cnt ? cnt - 1u : 0u) | (legal0 << 16), 0u);
         }
     }
     HIPCHK(c, hipMalloc(&c->t_row1, sizeof(uint4) * P));

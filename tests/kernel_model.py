@@ -77,16 +77,17 @@ class KernelModel:
         return m
 
     def _legal_w1(self, e):
-        """Env<1, TB>::legal_mask: one rotated 32-bit window over the padded 64-bit blocked board."""
+        """Env<1, TB>::legal_mask: the free board (open, unvisited) stored one row up, shifted
+        right by the agent's bit; out-of-lattice neighbours read 0 (empty bottom row, padding
+        column, top row / bits shifted out of the 64-bit word)."""
         P, M = self.t.pitch, (1 << 64) - 1
         b = e["x"] * P + e["y"]
-        blk = (e["vis"] | (~e["open"] & M)) & M
-        r = (b - P) & 63                       # 64-bit rotate right: padding rows wrap below row 0
-        win = ((blk >> r) | (blk << (64 - r))) & 0xFFFFFFFF
-        w = ~win & 0xFFFFFFFF
+        fr = ((e["open"] & ~e["vis"]) << P) & M
+        w = (fr >> b) & 0xFFFFFFFF
         m = ((w >> (2 * P)) & 1) | (((w >> (P - 1)) & 1) << 1) | ((w & 1) << 2) | (((w >> (P + 1)) & 1) << 3)
-        if self.tb and (e["len"] >= 3 or (e["len"] == 2 and not e["pflags"] & 4)):
-            m |= 1 << (e["last"] ^ 2)
+        if self.tb:
+            bk = 0x7FFFFFFD + (0 if e["pflags"] & 4 else 1)   # (len + bk) >> 31: the traceback rule
+            m |= (((e["len"] + bk) & 0xFFFFFFFF) >> 31) << (e["last"] ^ 2)
         return m
 
     def _advance(self, e, a):
