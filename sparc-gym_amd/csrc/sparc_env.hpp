@@ -439,6 +439,10 @@ struct Env<1, TB, Stack> {
     uint32_t w = 0;      // window of fr at e (see above), valid between steps
     uint32_t pnr = 0;    // traceback: reversed move before the last one, read one step ahead
     uint32_t solved = 0, was_reset = 0;   // this step: a +1 outcome / an autoreset (for stats)
+    uint32_t rs = 0;     // the coming step is an autoreset step (its state already loaded)
+    // phase_move -> phase_trie hand-over: action, forward / pop, moved on a puzzle with
+    // solutions, done, reset step
+    uint32_t s_a = 0, s_fwd = 0, s_pop = 0, s_mv = 0, s_done = 0, s_rs = 0;
     uint4 rec;
 
     // all arms are computed unconditionally and merged with masks: a C++ ?: whose arms are
@@ -474,8 +478,16 @@ struct Env<1, TB, Stack> {
     // the current node's record, loaded unconditionally (L2-resident table); node <= trie_max
     // holds on validated tables, the clamp keeps a broken state from reading out of bounds
     __device__ __forceinline__ void load_rec(const Params& p) {
+#ifdef SPARC_DIAG_TRIE_FROM_LDS
+        // timing-only: the same gather from LDS (wrong records) to price the global latency
+        rec = reinterpret_cast<const uint4*>(diag_lds)[(trie_base + (node < trie_max ? node : trie_max)) & 1023u];
+#else
         rec = p.tab.trie[trie_base + (node < trie_max ? node : trie_max)];
+#endif
     }
+#ifdef SPARC_DIAG_TRIE_FROM_LDS
+    const uint8_t* diag_lds = nullptr;
+#endif
 
     // _load_puzzle (SPaRC_Gym.py:166-187) with fresh planes; step0 = -1 inside a rollout (the
     // same step's counter increment brings it to 0).  Inside a rollout the step that resets
@@ -494,6 +506,7 @@ struct Env<1, TB, Stack> {
         len = 1;
         node = 0;
         step = 0;
+        rs = 0;
         outcome = 0;
         pending = 0;
         rl = 0;
@@ -502,28 +515,33 @@ struct Env<1, TB, Stack> {
         load_rec(p);
     }
 
+    // ---- the step in two phases.  phase_move (legality, move, path, flags) needs no trie
+    // record; phase_trie (solution trie, reward) of step t needs the record gathered by
+    // phase_trie of step t-1.  k_rollout runs phase_trie(t-1) next to phase_move(t): two
+    // independent dependency chains per iteration, and a whole iteration for the gather.
+    // A step is: reset_next (if the previous step ended an episode) -> phase_move -> phase_trie.
+
+    // gymnasium next-step autoreset (reset(), SPaRC_Gym.py:1087): the step after a done step
+    // loads the next puzzle (index + 1 mod P), ignores its action and returns reward 0, flag
+    // 64.  Only the puzzle rows, the board and the counters are set here; the trie state is
+    // set to the root by that step's phase_trie (the done step's phase_trie still needs it).
     template <class Src>
-    __device__ __forceinline__ int advance(const Params& p, const Src& src, uint32_t a, uint32_t& flags) {
+    __device__ __forceinline__ void reset_next(const Params& p, const Src& src) {
+        if (pending & (uint32_t)(p.autoreset == 1)) {
+            reset_rows(src, pid + 1 == p.tab.num_puzzles ? 0u : pid + 1);
+            len = 1;
+            step = -1;   // this step's increment brings it to 0
+            rs = 1;
+        }
+    }
+
+    __device__ __forceinline__ uint32_t phase_move(const Params& p, uint32_t a) {
         const uint32_t P = p.pitch;
-        // gymnasium next-step autoreset (reset(), SPaRC_Gym.py:1087): the reset lanes run the
-        // same phases below as a no-move step (legal = 0) whose outputs are overridden
-#ifdef SPARC_DIAG_NO_RESET
-        const uint32_t live = ~0u;
-#else
-        const uint32_t live = (pending & (uint32_t)(p.autoreset == 1)) - 1u;   // 0 on reset lanes
-#endif
-        if (live == 0u) reset_rows(src, pid + 1 == p.tab.num_puzzles ? 0u : pid + 1);
-        // the rest of the reset as masks (no exec-masked merge block): len 1, root node, and
-        // step -1, which this step's increment brings to 0
-        len = (len & live) | (1u & ~live);
-        node &= live;
-        step = (int32_t)((uint32_t)step | ~live);
-        // ---- phase 1: move, free board, path, legality, flags (no trie record needed)
         step = __builtin_elementwise_add_sat(step, 1);                              // 1132
         const bool trunc0 = step >= p.max_steps;                                    // 1134
         // `action in legal` (1137): bit a of the legal mask; actions >= 4 read bit 4 (0); a
         // reset step does not move
-        const uint32_t moved = (legal >> (a < 4u ? a : 4u)) & live & 1u;
+        const uint32_t moved = (legal >> (a < 4u ? a : 4u)) & (rs ^ 1u) & 1u;
         // neighbour's bit in the window: right 2P, up P-1, left 0, down P+1 (bytes of one
         // constant; the bfe offset keeps 5 bits, so a<<3 selects byte a&3)
         const uint32_t pos = __builtin_amdgcn_ubfe(p.nbr_pos, a << 3, 8u);
@@ -542,35 +560,68 @@ struct Env<1, TB, Stack> {
         len = len + fwd - pop;
         e = moved ? e + pos - P : e;
         legal = legal_mask(P);
-        const bool term = (e == tgt) & (live != 0u);                                 // 1192
-        const bool trunc = (trunc0 | (legal == 0)) & !term & (live != 0u);          // 1195-1199
+        const bool live = rs == 0u;
+        const bool term = (e == tgt) & live;                                         // 1192
+        const bool trunc = (trunc0 | (legal == 0)) & !term & live;                  // 1195-1199
         const bool done = term | trunc;
-        flags = (legal << 2) | (live ? (uint32_t)term | ((uint32_t)trunc << 1) : 64u);
         pending = (uint32_t)done;
         if constexpr (TB) pnr = stk.read(__builtin_elementwise_sub_sat(len, 3u));   // next step's pop
-        __builtin_amdgcn_sched_barrier(0);
-        // ---- phase 2: solution trie (first read of the record loaded at the previous step)
+        s_a = a;
+        s_fwd = fwd;
+        s_pop = pop;
+        s_mv = moved & pflags & 1u;   // moved, and the puzzle has solutions (1205, 1217)
+        s_done = (uint32_t)done;
+        s_rs = rs;
+        rs = 0;
+        return (legal << 2) | (live ? (uint32_t)term | ((uint32_t)trunc << 1) : 64u);
+    }
+
+    __device__ __forceinline__ int phase_trie(const Params& p) {
+        // a reset step starts the new puzzle's trie at its root
+        const uint32_t rsm = 0u - s_rs;
+        node &= ~rsm;
+        off = pick(s_rs != 0u, ((pflags >> 1) & 1u) ^ 1u, off);
+        node_term = pick(s_rs != 0u, (pflags >> 3) & 1u, node_term);
+        // solution trie (first read of the record loaded at the previous step)
         const bool on = off == 0;
-        const uint32_t c = (uint32_t)((((uint64_t)rec.y << 32) | rec.x) >> ((a << 4) & 63u)) & 0xFFFFu;
-        const bool down = fwd & on & (c != kNone);
-        const bool up = pop & on;
-        node_term = pick(down, __builtin_amdgcn_ubfe(rec.z, 17u + a, 1u),
+        const uint32_t c = (uint32_t)((((uint64_t)rec.y << 32) | rec.x) >> ((s_a << 4) & 63u)) & 0xFFFFu;
+        const bool down = (s_fwd != 0u) & on & (c != kNone);
+        const bool up = (s_pop != 0u) & on;
+        node_term = pick(down, __builtin_amdgcn_ubfe(rec.z, 17u + s_a, 1u),
                          pick(up, rec_parent_term(rec), node_term));
         node = pick(down, c, pick(up, rec_parent(rec), node));
-        off = pick(on, (uint32_t)(fwd & (c == kNone)), off + fwd - pop);
+        off = pick(on, s_fwd & (uint32_t)(c == kNone), off + s_fwd - s_pop);
 #ifndef SPARC_DIAG_NO_TRIE_LOAD
         load_rec(p);
 #endif
-        // ---- phase 3: reward code (1204-1223): done: +100 on a solution, else -100 unless the
-        // previous done step already set outcome_reward = 1 (then 0); otherwise +-1 when moved
-        // (0 if the puzzle has no solutions); an autoreset step returns 0
+        // reward code (1204-1223): done: +100 on a solution, else -100 unless the previous
+        // done step already set outcome_reward = 1 (then 0); otherwise +-1 when moved (0 if the
+        // puzzle has no solutions); a reset step returns 0 (no move, not done)
         const bool match = (off == 0) & (node_term != 0);
+        const bool done = s_done != 0u;
         const int c_done = match ? 100 : (outcome != 1 ? -100 : 0);
-        const int c_move = (moved & pflags & 1u) ? (off == 0 ? 1 : -1) : 0;
+        const int c_move = s_mv ? (off == 0 ? 1 : -1) : 0;
         outcome = done ? ((match | (outcome == 1)) ? 1u : 2u) : 0u;
         solved = (uint32_t)(done & match);
-        was_reset = (uint32_t)(live == 0u);
         return done ? c_done : c_move;
+    }
+
+    // one whole step (k_step, and the generic-width interface)
+    template <class Src>
+    __device__ __forceinline__ int advance(const Params& p, const Src& src, uint32_t a, uint32_t& flags) {
+        reset_next(p, src);
+        flags = phase_move(p, a);
+        was_reset = s_rs;
+        return phase_trie(p);
+    }
+
+    // the code and solved flag that phase_trie would report again for the last step of the
+    // previous launch (k_rollout runs one phase_trie before its first step, on the stored
+    // state, which leaves the state unchanged; its outputs are subtracted from the stats)
+    __device__ __forceinline__ void replay_outputs(int& code, uint32_t& sol) const {
+        const bool match = (off == 0) & (node_term != 0);
+        code = pending ? (match ? 100 : (outcome != 1 ? -100 : 0)) : 0;
+        sol = (uint32_t)(pending & match);
     }
 
     template <class Src>
@@ -599,6 +650,10 @@ struct Env<1, TB, Stack> {
             rl = 0;
         }
         legal = legal_mask(P);
+        // a hand-over that replays the stored step's trie phase: no move, same done flag
+        rs = 0;
+        s_a = s_fwd = s_pop = s_mv = s_rs = 0;
+        s_done = pending;
     }
 
     template <class Src>

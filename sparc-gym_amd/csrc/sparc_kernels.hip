@@ -29,8 +29,9 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kTile = 16;                             // env-steps per LDS-transposed I/O tile
 constexpr int kWaves = kBlock / 64;
-// per-wave LDS I/O tiles (actions, reward codes, flags), EPW envs per wave
-template <int EPW>
+// per-wave LDS I/O tiles of the generic-width rollout (actions, reward codes, flags), EPW envs
+// per wave
+template <int W, int EPW>
 __host__ __device__ constexpr size_t tiles_lds_bytes() { return (size_t)kWaves * 3 * EPW * kTile; }
 constexpr size_t kMaxDynLds = 128 * 1024;
 
@@ -118,7 +119,7 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
     uint8_t* ta = smem + wv * (3 * EPW * kTile);
     uint8_t* tr = ta + EPW * kTile;
     uint8_t* tf = tr + EPW * kTile;
-    constexpr size_t kStackOff = tiles_lds_bytes<EPW>();
+    constexpr size_t kStackOff = tiles_lds_bytes<W, EPW>();
     constexpr size_t kTableOff = kStackOff + stack_lds_bytes<W, TB, EPW>();
     PuzzleSrc<W> src{p.tab.info, p.tab.root, p.tab.open, p.tab.init, p.tab.row1};
     if constexpr (LDS_TABLE) {
@@ -157,6 +158,9 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
     using Stack = typename std::conditional<(W == 1 && TB), LdsStack<EPW>, RegStack>::type;
     Env<W, TB, Stack> e;
     if constexpr (W == 1 && TB) e.stk.col = smem + kStackOff + wv * (64 * EPW) + lane;
+#ifdef SPARC_DIAG_TRIE_FROM_LDS
+    if constexpr (W == 1) e.diag_lds = smem + kTableOff;
+#endif
     if (active) e.load(p, src, i);
     int4 acc = make_int4(0, 0, 0, 0);
     u32x4 anext = {0u, 0u, 0u, 0u};
@@ -236,6 +240,185 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
         s.z += acc.z;
         s.w += acc.w;
         stats[i] = s;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// W = 1 rollout: 4 env waves + 1 I/O wave per workgroup (256 envs).
+//
+// The env waves only issue trie-record gathers to global memory.  Their vmcnt counter is in
+// order, so every wait for a gather would also wait for any older action prefetch or output
+// store; the I/O wave therefore moves all streamed data: it loads the action tile of tile k+1
+// into a double buffer and writes the reward / flag tiles of tile k-2 out of four-tile LDS
+// rings while the env waves step tile k, and one workgroup barrier per 16-step tile hands the
+// buffers over.  Env wave iteration t runs the trie phase of step t-1 next to the move phase
+// of step t (independent dependency chains; the gather issued in iteration t-1 has a whole
+// iteration to arrive).  Iteration 0's trie phase replays the stored step and changes
+// nothing; its outputs are subtracted from the stats.  Workgroups that are not full (or
+// unaligned I/O) step every env with per-step byte accesses and no I/O wave.
+constexpr int kBlock1 = 320;
+constexpr int kRing = 64;                              // output ring rows (4 tiles)
+constexpr size_t kW1Act = 2 * kTile * 64;              // per env wave: actions, double buffer
+constexpr size_t kW1Wave = kW1Act + 2 * kRing * 64 + 64 * 64;   // + reward / flag rings + move stack
+constexpr size_t kW1Base = 4 * kW1Wave;
+
+template <bool TB, bool RAND, bool LDS_TABLE>
+__global__ void __launch_bounds__(kBlock1) k_rollout1(Params p, int32_t T, const uint8_t* __restrict__ act,
+                                                      uint64_t seed, uint64_t t0, int8_t* __restrict__ rew,
+                                                      uint8_t* __restrict__ flg, int4* __restrict__ stats,
+                                                      uint32_t tiled) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    PuzzleSrc<1> src{p.tab.info, p.tab.root, p.tab.open, p.tab.init, p.tab.row1};
+    if constexpr (LDS_TABLE) {
+        const uint32_t P = p.tab.num_puzzles;
+        uint4* lrow1 = reinterpret_cast<uint4*>(smem + kW1Base);
+        uint64_t* linit = reinterpret_cast<uint64_t*>(lrow1 + P);
+        for (uint32_t k = threadIdx.x; k < P; k += kBlock1) {
+            lrow1[k] = p.tab.row1[k];
+            linit[k] = p.tab.init[k];
+        }
+        __syncthreads();
+        src = PuzzleSrc<1>{p.tab.info, p.tab.root, p.tab.open, linit, lrow1};
+    }
+    const size_t n = p.n;
+    const uint32_t wg_base = blockIdx.x * 256u;
+    const bool wg_full = tiled && (size_t)wg_base + 256 <= n;   // block-uniform
+    const int32_t K = wg_full ? T / kTile : 0;                   // full tiles
+    const uint32_t r = lane >> 2, c = (lane & 3u) * 16u;         // this lane's piece of a tile
+
+    if (wv == 4) {                                               // ---- the I/O wave
+        if (!wg_full) return;
+        auto load_tile = [&](int32_t k) {                        // actions of tile k -> buffer k & 1
+            if constexpr (!RAND) {
+                u32x4 v[4];
+#pragma unroll
+                for (int w = 0; w < 4; ++w) v[w] = nt_load16(act + (size_t)(k * kTile + r) * n + wg_base + w * 64 + c);
+#pragma unroll
+                for (int w = 0; w < 4; ++w)
+                    *reinterpret_cast<u32x4*>(smem + w * kW1Wave + (k & 1) * (kTile * 64) + r * 64 + c) = v[w];
+            }
+        };
+        auto store_tile = [&](int32_t k) {                       // tile k's outputs -> HBM
+            const uint32_t row = (uint32_t)((k * kTile) & (kRing - 1)) + r;
+            const size_t o = (size_t)(k * kTile + r) * n + wg_base + c;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const uint8_t* base = smem + w * kW1Wave + kW1Act;
+                if (rew) nt_store16(reinterpret_cast<uint8_t*>(rew) + o + w * 64,
+                                    *reinterpret_cast<const u32x4*>(base + row * 64 + c));
+                if (flg) nt_store16(flg + o + w * 64, *reinterpret_cast<const u32x4*>(base + kRing * 64 + row * 64 + c));
+            }
+        };
+#if defined(SPARC_DIAG_NO_BARRIER)
+        if (K > 0) load_tile(0);
+        __syncthreads();                                         // B_0
+#elif defined(SPARC_DIAG_IDLE_IO)
+        if (K > 0) load_tile(0);
+        __syncthreads();                                         // B_0
+        for (int32_t k = 0; k < K; ++k) __syncthreads();
+#else
+        if (K > 0) load_tile(0);
+        __syncthreads();                                         // B_0
+        for (int32_t k = 0; k < K; ++k) {
+            if (k + 1 < K) load_tile(k + 1);
+            if (k >= 2) store_tile(k - 2);
+            __syncthreads();                                     // B_{k+1}
+        }
+#endif
+        __syncthreads();                                         // B_end
+        if (K >= 2) store_tile(K - 2);
+        if (K >= 1) store_tile(K - 1);
+        return;
+    }
+
+    // ---- env waves
+    const uint32_t i = wg_base + wv * 64u + lane;
+    const bool active = i < n;
+    const uint64_t gid = p.env_offset + i;
+    uint8_t* wbase = smem + wv * kW1Wave;
+    uint8_t* tr = wbase + kW1Act;                                // reward ring [64][64]
+    uint8_t* tf = tr + kRing * 64;                               // flag ring [64][64]
+    using Stack = typename std::conditional<TB, LdsStack<64>, RegStack>::type;
+    Env<1, TB, Stack> e;
+    if constexpr (TB) e.stk.col = tf + kRing * 64 + lane;
+#ifdef SPARC_DIAG_TRIE_FROM_LDS
+    e.diag_lds = smem + kW1Base;
+#endif
+    int4 acc = make_int4(0, 0, 0, 0);
+    if (active) {
+        e.load(p, src, i);
+        int c0;
+        uint32_t s0;
+        e.replay_outputs(c0, s0);
+        acc.x -= c0;
+        acc.z -= (int)s0;
+    }
+    auto put_rew = [&](int32_t t, int code) {                   // reward code of step t
+        if (t < K * kTile) tr[(t & (kRing - 1)) * 64 + lane] = (uint8_t)code;
+        else if (rew) rew[(size_t)t * n + i] = (int8_t)code;
+    };
+    if (wg_full) __syncthreads();                                // B_0
+    for (int32_t k = 0; k < K; ++k) {
+        const uint8_t* ta = wbase + (k & 1) * (kTile * 64);
+#pragma unroll 1
+        for (int g = 0; g < kTile; g += 4) {
+            uint32_t av[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                av[j] = RAND ? uint_rand_action(seed, gid, t0 + (uint64_t)(k * kTile + g + j)) : ta[(g + j) * 64 + lane];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int32_t t = k * kTile + g + j;
+                e.reset_next(p, src);
+                const int code = e.phase_trie(p);
+#ifndef SPARC_DIAG_NO_OUT_LDS
+                tr[((t - 1) & (kRing - 1)) * 64 + lane] = (uint8_t)code;   // step t-1 (t = 0: unused row)
+#endif
+                const uint32_t f = e.phase_move(p, av[j]);
+#ifndef SPARC_DIAG_NO_OUT_LDS
+                tf[(t & (kRing - 1)) * 64 + lane] = (uint8_t)f;
+#endif
+#ifndef SPARC_DIAG_NO_STATS
+                acc.x += code;
+                acc.z += (int)e.solved;
+                acc.y += (int)e.pending;
+                acc.w += (int)e.s_rs;
+#endif
+            }
+        }
+#ifndef SPARC_DIAG_NO_BARRIER
+        __syncthreads();                                         // B_{k+1}
+#endif
+    }
+    if (active) {
+        for (int32_t t = K * kTile; t < T; ++t) {                // tail steps / partial workgroups
+            const uint32_t a = RAND ? uint_rand_action(seed, gid, t0 + (uint64_t)t) : act[(size_t)t * n + i];
+            e.reset_next(p, src);
+            const int code = e.phase_trie(p);
+            if (t > 0) put_rew(t - 1, code);
+            const uint32_t f = e.phase_move(p, a);
+            if (flg) flg[(size_t)t * n + i] = (uint8_t)f;
+            acc.x += code;
+            acc.z += (int)e.solved;
+            acc.y += (int)e.pending;
+            acc.w += (int)e.s_rs;
+        }
+        const int code = e.phase_trie(p);                        // the last step's trie phase
+        put_rew(T - 1, code);
+        acc.x += code;
+        acc.z += (int)e.solved;
+    }
+    if (wg_full) __syncthreads();                                // B_end: rings complete
+    if (!active) return;
+    e.store(p, src, i);
+    if (stats) {
+        int4 st = stats[i];
+        st.x += acc.x;
+        st.y += acc.y;
+        st.z += acc.z;
+        st.w += acc.w;
+        stats[i] = st;
     }
 }
 
@@ -671,15 +854,43 @@ int sparc_rollout_device(void* ctx, int32_t T, const uint8_t* d_act, uint64_t se
     // envs per wave: 64.  (Measured on MI355X at 65,536 envs: 32-wide waves, two per SIMD, are
     // 1.3x slower than one full wave per SIMD — a half-empty wave costs the full issue time.)
     const bool half = false;
+    if (c->W == 1) {
+        const size_t blocks = (c->n + 255) / 256;
+        const size_t per_cu = (blocks + 255) / 256;
+        const size_t budget = std::min(kMaxDynLds, (size_t)160 * 1024 / (per_cu ? per_cu : 1));
+        const size_t tbytes = table_lds_bytes<1>(c->num_puzzles);
+        const bool lds_table = kW1Base + tbytes <= budget;
+        const size_t shm = kW1Base + (lds_table ? tbytes : 0);
+        auto launch = [&](auto kern, const uint8_t* a) {
+            if (shm > 64 * 1024)
+                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+            kern<<<dim3((unsigned)blocks), kBlock1, shm, c->stream>>>(p, T, a, seed, t0, d_rew, d_flags, st, tiled);
+        };
+        auto go1 = [&](auto tb) {
+            constexpr bool TB = decltype(tb)::value;
+            if (d_act) {
+                if (lds_table) launch(k_rollout1<TB, false, true>, d_act);
+                else launch(k_rollout1<TB, false, false>, d_act);
+            } else {
+                if (lds_table) launch(k_rollout1<TB, true, true>, nullptr);
+                else launch(k_rollout1<TB, true, false>, nullptr);
+            }
+        };
+        if (c->cfg.traceback) go1(std::true_type{});
+        else go1(std::false_type{});
+        return launch_check(c);
+    }
     dispatch_w_tb(c->W, c->cfg.traceback, [&](auto w, auto tb) {
         constexpr int W = decltype(w)::value;
         constexpr bool TB = decltype(tb)::value;
+        if constexpr (W == 1) return;   // k_rollout1 above
         auto go = [&](auto epw_c) {
             constexpr int EPW = decltype(epw_c)::value;
             const size_t blocks = (c->n + kWaves * EPW - 1) / (kWaves * EPW);
             const size_t per_cu = (blocks + 255) / 256;
             const size_t budget = std::min(kMaxDynLds, (size_t)160 * 1024 / (per_cu ? per_cu : 1));
-            const size_t base = tiles_lds_bytes<EPW>() + stack_lds_bytes<W, TB, EPW>();
+            const size_t base = tiles_lds_bytes<W, EPW>() + stack_lds_bytes<W, TB, EPW>();
             const size_t tbytes = table_lds_bytes<W>(c->num_puzzles);
             const bool lds_table = base + tbytes <= budget;
             const size_t shm = base + (lds_table ? tbytes : 0);

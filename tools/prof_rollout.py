@@ -9,6 +9,9 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "sparc-gym_amd"))
 
+if "--lib" in sys.argv:   # a diagnostic build of the library (set before the package loads it)
+    os.environ["SPARC_DIAG_LIB"] = os.path.abspath(sys.argv[sys.argv.index("--lib") + 1])
+
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
@@ -24,6 +27,7 @@ ap.add_argument("--launches", type=int, default=4)
 ap.add_argument("--rand", action="store_true", help="in-kernel counter-based actions (no action loads)")
 ap.add_argument("--no-out", action="store_true", help="do not write reward codes / flags")
 ap.add_argument("--time", action="store_true", help="print the mean launch time (HIP events)")
+ap.add_argument("--lib", default=None, help="path of a diagnostic build of libsparc_gym_amd.so")
 a = ap.parse_args()
 sizes, full, tb = bench.CONFIGS[a.config]
 proc = process_puzzles(synthetic.make_puzzles(1024, seed=0, sizes=sizes, full_properties=full))
