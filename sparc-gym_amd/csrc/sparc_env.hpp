@@ -49,6 +49,7 @@ struct Table {
     const uint4* __restrict__ trie;     // [nodes]
     const uint64_t* __restrict__ init;  // [P] padded W = 1 layout: blocked board at reset
     const uint4* __restrict__ row1;     // [P] padded W = 1 layout: compact puzzle row
+    const uint4* __restrict__ trie1;    // [nodes] W = 1 layout: packed nodes (see Env<1>)
     uint32_t num_puzzles;
 };
 
@@ -432,7 +433,8 @@ template <bool TB, class Stack>
 struct Env<1, TB, Stack> {
     uint64_t fr;         // free board, one row up (bit e + pitch = point e)
     Stack stk;           // reversed moves of self.path (traceback only)
-    uint32_t e, len, off, node, node_term, outcome, pending, pid, legal, rl;
+    uint32_t e, len, off, outcome, pending, pid, legal, rl;
+    uint32_t nn;         // trie node | node_term << 15 (a "packed node", as in the W = 1 records)
     int32_t step;
     uint32_t tgt, pflags, trie_base, trie_max;
     uint32_t bk;         // traceback rule bias: (len + bk) >> 31 = len >= 3 or (len == 2, open start)
@@ -475,14 +477,16 @@ struct Env<1, TB, Stack> {
         return r.x & 0xFFu;   // start
     }
 
-    // the current node's record, loaded unconditionally (L2-resident table); node <= trie_max
-    // holds on validated tables, the clamp keeps a broken state from reading out of bounds
+    // the current node's record, loaded unconditionally (L2-resident table).  W = 1 records
+    // (trie1): x = child[right] | child[up] << 16, y = child[left] | child[down] << 16,
+    // z = parent, each a packed node (index | terminal << 15, 0xFFFF = none).  node <= trie_max
+    // holds on validated tables; the clamp keeps a broken state from reading out of bounds.
     __device__ __forceinline__ void load_rec(const Params& p) {
+        const uint32_t node = nn & 0x7FFFu;
 #ifdef SPARC_DIAG_TRIE_FROM_LDS
-        // timing-only: the same gather from LDS (wrong records) to price the global latency
         rec = reinterpret_cast<const uint4*>(diag_lds)[(trie_base + (node < trie_max ? node : trie_max)) & 1023u];
 #else
-        rec = p.tab.trie[trie_base + (node < trie_max ? node : trie_max)];
+        rec = p.tab.trie1[trie_base + (node < trie_max ? node : trie_max)];
 #endif
     }
 #ifdef SPARC_DIAG_TRIE_FROM_LDS
@@ -498,13 +502,12 @@ struct Env<1, TB, Stack> {
         e = load_puzzle(src, q);
         fr = src.get_init(q);
         off = ((pflags >> 1) & 1u) ^ 1u;
-        node_term = (pflags >> 3) & 1u;   // the root is itself a solution ([start])
     }
     template <class Src>
     __device__ __forceinline__ void reset(const Params& p, const Src& src, uint32_t q) {
         reset_rows(src, q);
         len = 1;
-        node = 0;
+        nn = ((pflags >> 3) & 1u) << 15;   // node 0 (the root); it is a solution iff [start] is one
         step = 0;
         rs = 0;
         outcome = 0;
@@ -560,44 +563,44 @@ struct Env<1, TB, Stack> {
         len = len + fwd - pop;
         e = moved ? e + pos - P : e;
         legal = legal_mask(P);
-        const bool live = rs == 0u;
-        const bool term = (e == tgt) & live;                                         // 1192
-        const bool trunc = (trunc0 | (legal == 0)) & !term & live;                  // 1195-1199
-        const bool done = term | trunc;
-        pending = (uint32_t)done;
+        const uint32_t live = rs ^ 1u;                                               // 0 on a reset step
+        const uint32_t term = e == tgt ? live : 0u;                                  // 1192
+        const uint32_t trunc = (trunc0 | (legal == 0)) ? live ^ term : 0u;          // 1195-1199
+        const uint32_t done = term | trunc;
+        pending = done;
         if constexpr (TB) pnr = stk.read(__builtin_elementwise_sub_sat(len, 3u));   // next step's pop
         s_a = a;
         s_fwd = fwd;
         s_pop = pop;
         s_mv = moved & pflags & 1u;   // moved, and the puzzle has solutions (1205, 1217)
-        s_done = (uint32_t)done;
+        s_done = done;
         s_rs = rs;
+        const uint32_t f = (legal << 2) | (rs << 6) | term | (trunc << 1);
         rs = 0;
-        return (legal << 2) | (live ? (uint32_t)term | ((uint32_t)trunc << 1) : 64u);
+        return f;
     }
 
     __device__ __forceinline__ int phase_trie(const Params& p) {
         // a reset step starts the new puzzle's trie at its root
-        const uint32_t rsm = 0u - s_rs;
-        node &= ~rsm;
+        nn = pick(s_rs != 0u, ((pflags >> 3) & 1u) << 15, nn);
         off = pick(s_rs != 0u, ((pflags >> 1) & 1u) ^ 1u, off);
-        node_term = pick(s_rs != 0u, (pflags >> 3) & 1u, node_term);
-        // solution trie (first read of the record loaded at the previous step)
+        // solution trie (first read of the record loaded at the previous step): a forward move
+        // on the trie goes to the child (or leaves the trie), a pop on the trie to the parent,
+        // off the trie they count the depth off it
         const bool on = off == 0;
         const uint32_t c = (uint32_t)((((uint64_t)rec.y << 32) | rec.x) >> ((s_a << 4) & 63u)) & 0xFFFFu;
-        const bool down = (s_fwd != 0u) & on & (c != kNone);
+        const bool has = c != 0xFFFFu;
+        const bool down = (s_fwd != 0u) & on & has;
         const bool up = (s_pop != 0u) & on;
-        node_term = pick(down, __builtin_amdgcn_ubfe(rec.z, 17u + s_a, 1u),
-                         pick(up, rec_parent_term(rec), node_term));
-        node = pick(down, c, pick(up, rec_parent(rec), node));
-        off = pick(on, s_fwd & (uint32_t)(c == kNone), off + s_fwd - s_pop);
+        nn = pick(down, c, pick(up, rec.z, nn));
+        off = pick(on, s_fwd & (uint32_t)!has, off + s_fwd - s_pop);
 #ifndef SPARC_DIAG_NO_TRIE_LOAD
         load_rec(p);
 #endif
         // reward code (1204-1223): done: +100 on a solution, else -100 unless the previous
         // done step already set outcome_reward = 1 (then 0); otherwise +-1 when moved (0 if the
         // puzzle has no solutions); a reset step returns 0 (no move, not done)
-        const bool match = (off == 0) & (node_term != 0);
+        const bool match = (off == 0) & (nn >= 0x8000u);
         const bool done = s_done != 0u;
         const int c_done = match ? 100 : (outcome != 1 ? -100 : 0);
         const int c_move = s_mv ? (off == 0 ? 1 : -1) : 0;
@@ -619,7 +622,7 @@ struct Env<1, TB, Stack> {
     // previous launch (k_rollout runs one phase_trie before its first step, on the stored
     // state, which leaves the state unchanged; its outputs are subtracted from the stats)
     __device__ __forceinline__ void replay_outputs(int& code, uint32_t& sol) const {
-        const bool match = (off == 0) & (node_term != 0);
+        const bool match = (off == 0) & (nn >= 0x8000u);
         code = pending ? (match ? 100 : (outcome != 1 ? -100 : 0)) : 0;
         sol = (uint32_t)(pending & match);
     }
@@ -633,10 +636,9 @@ struct Env<1, TB, Stack> {
         e = (ps & 0xFFu) * P + ((ps >> 8) & 0xFFu);
         len = (ps >> 16) & 0xFFu;
         off = ps >> 24;
-        node = ax & 0xFFFFu;
+        nn = (ax & 0x7FFFu) | (((ax >> 19) & 1u) << 15);
         outcome = (ax >> 16) & 3u;
         pending = (ax >> 18) & 1u;
-        node_term = (ax >> 19) & 1u;
         step = (int32_t)s.step[i];
         pid = s.pid[i];
         load_puzzle(src, pid);
@@ -667,7 +669,7 @@ struct Env<1, TB, Stack> {
         if constexpr (TB) stk.store(s.dirs, p.n, i, len >= 1 ? len - 1 : 0u);
         const uint32_t x = e / P, y = e - x * P;
         s.pos[i] = x | (y << 8) | (len << 16) | (off << 24);
-        s.aux[i] = node | (outcome << 16) | (pending << 18) | (node_term << 19);
+        s.aux[i] = (nn & 0x7FFFu) | (outcome << 16) | (pending << 18) | ((nn >> 15) << 19);
         s.step[i] = (uint32_t)step;
         s.pid[i] = pid;
     }

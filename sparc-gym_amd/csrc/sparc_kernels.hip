@@ -475,7 +475,7 @@ struct Ctx {
     uint64_t *vis = nullptr, *dirs = nullptr;
     uint32_t *pos = nullptr, *aux = nullptr, *step = nullptr, *pid = nullptr;
     uint64_t* t_open = nullptr;
-    uint4 *t_info = nullptr, *t_root = nullptr, *t_trie = nullptr;
+    uint4 *t_info = nullptr, *t_root = nullptr, *t_trie = nullptr, *t_trie1 = nullptr;
     uint64_t* t_init = nullptr;
     uint4* t_row1 = nullptr;
     int32_t* err = nullptr;
@@ -515,6 +515,7 @@ Params make_params(const Ctx* c) {
     p.tab.info = c->t_info;
     p.tab.root = c->t_root;
     p.tab.trie = c->t_trie;
+    p.tab.trie1 = c->t_trie1;
     p.tab.init = c->t_init;
     p.tab.row1 = c->t_row1;
     p.tab.num_puzzles = c->num_puzzles;
@@ -621,7 +622,7 @@ int sparc_destroy(void* ctx) {
     if (!c) return SPARC_OK;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void* bufs[] = {c->vis, c->dirs, c->pos, c->aux, c->step, c->pid, c->t_open, c->t_info, c->t_root, c->t_trie, c->t_init, c->t_row1,
+    void* bufs[] = {c->vis, c->dirs, c->pos, c->aux, c->step, c->pid, c->t_open, c->t_info, c->t_root, c->t_trie, c->t_trie1, c->t_init, c->t_row1,
                     c->err, c->s_act, c->s_flags, c->s_mask, c->s_rew, c->s_pidx, c->r_planes, c->r_inst_range,
                     c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off, c->s_bits, c->s_region, c->s_fit};
     for (void* b : bufs)
@@ -688,7 +689,7 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
             snprintf(m, sizeof m, "puzzle %d: start/target outside the lattice", q);
             return fail(c, SPARC_E_INVALID, m);
         }
-        if ((fl & 2u) && (cnt == 0 || (uint64_t)base + cnt > (uint64_t)t->num_nodes || cnt > 0xFFFF)) {
+        if ((fl & 2u) && (cnt == 0 || (uint64_t)base + cnt > (uint64_t)t->num_nodes || cnt > (W == 1 ? 0x7FFFu : 0xFFFFu))) {
             snprintf(m, sizeof m, "puzzle %d: trie range out of bounds", q);
             return fail(c, SPARC_E_INVALID, m);
         }
@@ -708,6 +709,8 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
     if (c->t_open) HIPCHK(c, hipFree(c->t_open));
     if (c->t_info) HIPCHK(c, hipFree(c->t_info));
     if (c->t_trie) HIPCHK(c, hipFree(c->t_trie));
+    if (c->t_trie1) HIPCHK(c, hipFree(c->t_trie1));
+    c->t_trie1 = nullptr;
     if (c->t_root) HIPCHK(c, hipFree(c->t_root));
     if (c->t_init) HIPCHK(c, hipFree(c->t_init));
     if (c->t_row1) HIPCHK(c, hipFree(c->t_row1));
@@ -772,6 +775,22 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
     HIPCHK(c, hipMemset(c->t_trie, 0xFF, sizeof(uint4) * nn));
     if (t->num_nodes > 0)
         HIPCHK(c, hipMemcpy(c->t_trie, t->trie, sizeof(uint4) * (size_t)t->num_nodes, hipMemcpyHostToDevice));
+    if (W == 1) {
+        // packed-node records of Env<1>: every child and the parent as index | terminal << 15
+        // (0xFFFF = none), so one 16-bit field carries both a node and its terminal flag
+        std::vector<uint4> t1(nn, make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFu, 0u));
+        for (size_t k = 0; k < (size_t)t->num_nodes; ++k) {
+            const uint32_t* r = t->trie + 4 * k;
+            uint32_t ch[4] = {r[0] & 0xFFFFu, r[0] >> 16, r[1] & 0xFFFFu, r[1] >> 16};
+            for (int d = 0; d < 4; ++d)
+                if (ch[d] != 0xFFFFu) ch[d] |= ((r[2] >> (17 + d)) & 1u) << 15;
+            uint32_t par = r[2] & 0xFFFFu;
+            if (par != 0xFFFFu) par |= ((r[2] >> 21) & 1u) << 15;
+            t1[k] = make_uint4(ch[0] | (ch[1] << 16), ch[2] | (ch[3] << 16), par, 0u);
+        }
+        HIPCHK(c, hipMalloc(&c->t_trie1, sizeof(uint4) * nn));
+        HIPCHK(c, hipMemcpy(c->t_trie1, t1.data(), sizeof(uint4) * nn, hipMemcpyHostToDevice));
+    }
     c->num_puzzles = (uint32_t)t->num_puzzles;
     c->num_nodes = (uint32_t)t->num_nodes;
     c->loaded = true;
