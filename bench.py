@@ -208,7 +208,7 @@ def main():
     per_env_launch = 2 * sb + (32 if args.mode == "rollout" else 0)
     bytes_launch = n * (3 * avg_T + per_env_launch)
     achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
-    kernel = "k_rollout" if args.mode == "rollout" else "k_step"
+    kernel = ("k_rollout1" if table.words == 1 else "k_rollout") if args.mode == "rollout" else "k_step"
     workload = f"{args.config}_{args.mode}_n{n}_chunk{chunk if args.mode == 'rollout' else 1}"
     traffic = load_traffic(workload, kernel)
     out = {

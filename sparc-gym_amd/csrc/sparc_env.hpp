@@ -551,9 +551,10 @@ struct Env<1, TB, Stack> {
         // the only legal move onto a non-free point is the traceback pop (1141-1166)
         const uint32_t pop = TB ? moved & ~__builtin_amdgcn_ubfe(w, pos, 1u) : 0u;
         const uint32_t fwd = moved ^ pop;                                            // 1167-1188
-        // free board: a forward move takes the target (bit e + pos), a pop frees the point it
-        // leaves (bit e + P)
-        const uint32_t tog = e + (fwd ? pos : P);
+        const uint32_t d = pos - P;                  // the neighbour's offset from e
+        // free board: a forward move takes the target (bit e + d + P), a pop frees the point
+        // it leaves (bit e + P)
+        const uint32_t tog = e + P + (fwd ? d : 0u);
         fr ^= (uint64_t)moved << (tog & 63u);
         if constexpr (TB) {
             const uint32_t ar = a ^ 2u;
@@ -561,7 +562,7 @@ struct Env<1, TB, Stack> {
             rl = fwd ? ar : (pop ? pnr : rl);
         }
         len = len + fwd - pop;
-        e = moved ? e + pos - P : e;
+        e += moved ? d : 0u;
         legal = legal_mask(P);
         const uint32_t live = rs ^ 1u;                                               // 0 on a reset step
         const uint32_t term = e == tgt ? live : 0u;                                  // 1192

@@ -88,7 +88,11 @@ __device__ __forceinline__ u32x4 nt_load16(const uint8_t* q) {
     return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(q));
 }
 __device__ __forceinline__ void nt_store16(uint8_t* q, u32x4 v) {
+#ifdef SPARC_EXP_STORE_NO_NT
+    *reinterpret_cast<u32x4*>(q) = v;
+#else
     __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(q));
+#endif
 }
 
 // orders one wave's LDS accesses across its lanes (a wave's DS instructions execute in order;
@@ -299,15 +303,21 @@ __global__ void __launch_bounds__(kBlock1) k_rollout1(Params p, int32_t T, const
                     *reinterpret_cast<u32x4*>(smem + w * kW1Wave + (k & 1) * (kTile * 64) + r * 64 + c) = v[w];
             }
         };
-        auto store_tile = [&](int32_t k) {                       // tile k's outputs -> HBM
-            const uint32_t row = (uint32_t)((k * kTile) & (kRing - 1)) + r;
-            const size_t o = (size_t)(k * kTile + r) * n + wg_base + c;
+        // tile k's outputs -> HBM: each store instruction covers 8 rows x 128 B (two env waves'
+        // row segments), whole 128-B lines, so no partial-line writes reach HBM
+        auto store_tile = [&](int32_t k) {
+            const uint32_t r8 = lane >> 3, c8 = (lane & 7u) * 16u;     // row / byte of this lane
 #pragma unroll
-            for (int w = 0; w < 4; ++w) {
-                const uint8_t* base = smem + w * kW1Wave + kW1Act;
-                if (rew) nt_store16(reinterpret_cast<uint8_t*>(rew) + o + w * 64,
-                                    *reinterpret_cast<const u32x4*>(base + row * 64 + c));
-                if (flg) nt_store16(flg + o + w * 64, *reinterpret_cast<const u32x4*>(base + kRing * 64 + row * 64 + c));
+            for (int h = 0; h < 2; ++h) {
+                const uint32_t row = (uint32_t)((k * kTile) & (kRing - 1)) + h * 8 + r8;
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const int w = 2 * q + (int)(c8 >> 6);
+                    const uint8_t* base = smem + w * kW1Wave + kW1Act + row * 64 + (c8 & 63u);
+                    const size_t o = (size_t)(k * kTile + h * 8 + r8) * n + wg_base + q * 128 + c8;
+                    if (rew) nt_store16(reinterpret_cast<uint8_t*>(rew) + o, *reinterpret_cast<const u32x4*>(base));
+                    if (flg) nt_store16(flg + o, *reinterpret_cast<const u32x4*>(base + kRing * 64));
+                }
             }
         };
 #if defined(SPARC_DIAG_NO_BARRIER)
