@@ -169,7 +169,7 @@ int sparc_state_ptr(void *ctx, int32_t which, void **d_ptr);
  *              cells with count > 0 (x in 1..x_size-2, y in 1..y_size-2) and their count bits
  *              0-2 (count clamped to 7), star, square, coloured, colour 1..8, per-cell symbol
  *              multiplicity bits 0-2 (layers other than visited/gaps/agent/target set at a
- *              cell), y != 0, y != y_size-1
+ *              cell), y != 0, y != y_size-1, cells holding a poly/ylop instance
  *  inst_range  [P] first | count << 16 into inst (poly/ylop instances at cell centres,
  *              _extract_poly_instances 714-734)
  *  inst        bit | ylop << 10 | cx << 11 | cy << 14 | shape << 17
@@ -177,7 +177,7 @@ int sparc_state_ptr(void *ctx, int32_t which, void **d_ptr);
  *              shape array (722); shape_off [offsets][2] = (dx, dy) in cell units relative to
  *              the shape's anchor (_get_offsets 840-855)
  * Limits per puzzle: 16 ylops, 64 polys, 16 distinct poly shapes, lattice <= 15 x 15.         */
-#define SPARC_RULE_PLANES 24
+#define SPARC_RULE_PLANES 25
 typedef struct {
     int32_t num_puzzles;    /* must equal the loaded step table's */
     int32_t num_inst;

@@ -36,7 +36,7 @@ constexpr uint32_t kErrRuleSearch = 4, kErrRuleTable = 8;
 // rule-plane indices of include/sparc_gym_amd.h (SPARC_RULE_PLANES)
 enum : uint32_t {
     RP_CELLS = 0, RP_LATTICE, RP_GAPS, RP_DOTS, RP_TRI, RP_TRI0, RP_TRI1, RP_TRI2, RP_STAR, RP_SQUARE,
-    RP_COLORED, RP_COL1, RP_M0 = RP_COL1 + 8, RP_M1, RP_M2, RP_NOTFIRST, RP_NOTLAST, RP_COUNT
+    RP_COLORED, RP_COL1, RP_M0 = RP_COL1 + 8, RP_M1, RP_M2, RP_NOTFIRST, RP_NOTLAST, RP_INST, RP_COUNT
 };
 constexpr int kFitCells = 64;     // cell grid of the exact fit (15 x 15 lattice: 7 x 7 = 49)
 constexpr int kFitYlops = 16;     // per puzzle limits, validated by the loader
@@ -96,44 +96,70 @@ struct FitIn {
 };
 
 // ---------------------------------------------------------------- exact fit (736-838)
-__device__ __forceinline__ bool fit_place(int8_t* g, const RulesTab& rt, uint32_t shape, int a, uint32_t CX,
-                                          uint32_t CY, int sign) {
-    const uint32_t sr = rt.shape_range[shape];
+// The search runs on the cell grid (CX x CY <= 7 x 7 cells, bit cx*CY + cy of a u64: the
+// reference's row-major order, so "the first negative cell" is the lowest set bit).  Cell
+// counts are two's-complement bit-sliced counters (kFitPlanes planes, -32..31 >= -(1 + 16
+// ylops)); placing a shape adds or subtracts its cell mask with a ripple over the planes.  A
+// shape is its cell pattern relative to its anchor (the shape's first cell in row-major order,
+// _get_offsets 840-855) plus the set of anchors at which it fits the grid (_try_place_polys
+// 858-871).
+constexpr int kFitPlanes = 6;
+struct FitGrid {
+    uint64_t p[kFitPlanes];
+    __device__ __forceinline__ void add(uint64_t m) {
+#pragma unroll
+        for (int i = 0; i < kFitPlanes; ++i) { const uint64_t t = p[i] & m; p[i] ^= m; m = t; }
+    }
+    __device__ __forceinline__ void sub(uint64_t m) {
+#pragma unroll
+        for (int i = 0; i < kFitPlanes; ++i) { const uint64_t t = ~p[i] & m; p[i] ^= m; m = t; }
+    }
+    __device__ __forceinline__ uint64_t neg() const { return p[kFitPlanes - 1]; }
+    __device__ __forceinline__ uint64_t nonzero() const {
+        uint64_t a = 0;
+#pragma unroll
+        for (int i = 0; i < kFitPlanes; ++i) a |= p[i];
+        return a;
+    }
+};
+
+// pattern (relative to the anchor) and fitting anchors of shape `sh` on a CX x CY cell grid
+__device__ __forceinline__ void fit_shape(const RulesTab& rt, uint32_t sh, uint32_t CX, uint32_t CY, uint64_t& pat,
+                                          uint64_t& va) {
+    const uint32_t sr = rt.shape_range[sh];
     const uint32_t o0 = sr & 0xFFFFu, n = sr >> 16;
-    const int ax = a / (int)CY, ay = a - ax * (int)CY;
-    for (uint32_t k = 0; k < n; ++k) {   // _try_place_polys: all targets in bounds first
-        const int tx = ax + rt.shape_off[2 * (o0 + k)], ty = ay + rt.shape_off[2 * (o0 + k) + 1];
-        if (tx < 0 || tx >= (int)CX || ty < 0 || ty >= (int)CY) return false;
-    }
+    int mdx = 0, mdy0 = 0, mdy1 = 0;
+    pat = 0;
+    bool ok = true;
     for (uint32_t k = 0; k < n; ++k) {
-        const int tx = ax + rt.shape_off[2 * (o0 + k)], ty = ay + rt.shape_off[2 * (o0 + k) + 1];
-        g[tx * (int)CY + ty] += (int8_t)sign;
+        const int dx = rt.shape_off[2 * (o0 + k)], dy = rt.shape_off[2 * (o0 + k) + 1];
+        mdx = dx > mdx ? dx : mdx;
+        mdy0 = dy < mdy0 ? dy : mdy0;
+        mdy1 = dy > mdy1 ? dy : mdy1;
+        const int lin = dx * (int)CY + dy;
+        if (lin < 0 || lin > 63) ok = false;
+        else pat |= 1ull << lin;
     }
-    return true;
+    va = 0;
+    if (!ok) return;   // wider than the grid: it fits nowhere
+    for (int ax = 0; ax + mdx < (int)CX; ++ax)
+        for (int ay = -mdy0; ay + mdy1 < (int)CY; ++ay) va |= 1ull << (ax * (int)CY + ay);
 }
 
-__device__ __forceinline__ void fit_unplace(int8_t* g, const RulesTab& rt, uint32_t shape, int a, uint32_t CY,
-                                            int sign) {
-    const uint32_t sr = rt.shape_range[shape];
-    const uint32_t o0 = sr & 0xFFFFu, n = sr >> 16;
-    const int ax = a / (int)CY, ay = a - ax * (int)CY;
-    for (uint32_t k = 0; k < n; ++k) {
-        const int tx = ax + rt.shape_off[2 * (o0 + k)], ty = ay + rt.shape_off[2 * (o0 + k) + 1];
-        g[tx * (int)CY + ty] -= (int8_t)sign;
-    }
-}
-
-// _polyfit_region_exact with area already equal (so net = area > 0 and the grid starts at -1
-// on the region's cells).  region_cell(k) tells whether cell k (= cx*CY + cy) is in the region.
+// _polyfit_region_exact with the area check passed (so net = area > 0 and the grid starts at
+// -1 on the region's cells), as a depth-first search over the same choices (existence only:
+// identical ylops take non-decreasing anchors, polys are tried by distinct shape)
 template <int W>
 __device__ __noinline__ bool exact_fit(const FitIn& in, const BB<W>& Rc, uint32_t pitch, int32_t* err) {
     const RulesTab& rt = *in.rt;
-    const int NC = (int)(in.CX * in.CY);
-    int8_t g[kFitCells];
-    for (int k = 0; k < NC; ++k) {
-        const uint32_t cx = (uint32_t)k / in.CY, cy = (uint32_t)k - cx * in.CY;
-        g[k] = Rc.test((2 * cx + 1) * pitch + 2 * cy + 1) ? (int8_t)-1 : (int8_t)0;
-    }
+    const uint32_t CX = in.CX, CY = in.CY;
+    FitGrid g;
+    uint64_t rm = 0;
+    for (uint32_t cx = 0; cx < CX; ++cx)
+        for (uint32_t cy = 0; cy < CY; ++cy)
+            if (Rc.test((2 * cx + 1) * pitch + 2 * cy + 1)) rm |= 1ull << (cx * CY + cy);
+#pragma unroll
+    for (int i = 0; i < kFitPlanes; ++i) g.p[i] = rm;    // -1 on the region
     uint32_t ysh[kFitYlops], dsh[kFitShapes];
     int cnt[kFitShapes];
     int ny = 0, nd = 0, np = 0;
@@ -153,6 +179,9 @@ __device__ __noinline__ bool exact_fit(const FitIn& in, const BB<W>& Rc, uint32_
             ++np;
         }
     }
+    uint64_t ypat[kFitYlops], yva[kFitYlops], dpat[kFitShapes], dva[kFitShapes];
+    for (int k = 0; k < ny; ++k) fit_shape(rt, ysh[k], CX, CY, ypat[k], yva[k]);
+    for (int k = 0; k < nd; ++k) fit_shape(rt, dsh[k], CX, CY, dpat[k], dva[k]);
     int cur[kFitYlops + kFitDepth + 1];
     int pat[kFitDepth + 1];
     const int LMAX = ny + np;
@@ -163,15 +192,17 @@ __device__ __noinline__ bool exact_fit(const FitIn& in, const BB<W>& Rc, uint32_
         if (++iters > kFitCap) { atomicOr(err, (int)kErrRuleSearch); return false; }
         if (L < ny) {                                            // _polyfit_place_ylops
             int a = cur[L];
-            if (a >= 0) fit_unplace(g, rt, ysh[L], a, in.CY, -1);
+            if (a >= 0) g.add(ypat[L] << a);
             a = a < 0 ? ((L > 0 && ysh[L] == ysh[L - 1]) ? cur[L - 1] : 0) : a + 1;
-            while (a < NC && !fit_place(g, rt, ysh[L], a, in.CX, in.CY, -1)) ++a;
-            if (a >= NC) {
+            const uint64_t cand = a < 64 ? yva[L] & (~0ull << a) : 0ull;
+            if (!cand) {
                 cur[L] = -1;
                 if (L == 0) return false;
                 --L;
                 continue;
             }
+            a = __ffsll((long long)cand) - 1;
+            g.sub(ypat[L] << a);
             cur[L] = a;
             cur[++L] = -1;
             continue;
@@ -179,36 +210,32 @@ __device__ __noinline__ bool exact_fit(const FitIn& in, const BB<W>& Rc, uint32_
         const int lv = L - ny;                                   // _polyfit_place_polys
         int j = cur[L];
         if (j < 0) {
-            bool pos = false, neg = false;
-            int t = -1;
-            for (int k = 0; k < NC; ++k) {
-                pos |= g[k] > 0;
-                if (g[k] < 0 && t < 0) t = k;
-            }
-            neg = t >= 0;
+            const uint64_t ng = g.neg();
+            const bool pos = (g.nonzero() & ~ng) != 0;
             bool done = false, ok = false;
             if (pos) done = true;                                // any(grid > 0): False
-            else if (L == LMAX) { done = true; ok = !neg; }       // no polys left
-            else if (!neg) { done = true; ok = true; }           // no negative cell: True
+            else if (L == LMAX) { done = true; ok = ng == 0; }    // no polys left
+            else if (ng == 0) { done = true; ok = true; }        // no negative cell: True
             if (done) {
                 if (ok) return true;
                 if (L == 0) return false;
                 --L;
                 continue;
             }
-            pat[lv] = t;
+            pat[lv] = __ffsll((long long)ng) - 1;               // the first negative cell
         } else {
-            fit_unplace(g, rt, dsh[j], pat[lv], in.CY, +1);
+            g.sub(dpat[j] << pat[lv]);
             ++cnt[j];
         }
         ++j;
-        while (j < nd && (cnt[j] == 0 || !fit_place(g, rt, dsh[j], pat[lv], in.CX, in.CY, +1))) ++j;
+        while (j < nd && (cnt[j] == 0 || !((dva[j] >> pat[lv]) & 1ull))) ++j;
         if (j >= nd) {
             cur[L] = -1;
             if (L == 0) return false;
             --L;
             continue;
         }
+        g.add(dpat[j] << pat[lv]);
         --cnt[j];
         cur[L] = j;
         cur[++L] = -1;
@@ -226,15 +253,21 @@ struct RuleOut {
 template <int W>
 __device__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const BB<W>& vis, uint32_t x, uint32_t y,
                             uint32_t q, uint8_t* region_out) {
-    const uint64_t* pl = rt.planes + (size_t)q * RP_COUNT * W;
+    // every plane of the puzzle in registers up front: one round of loads, none in the loops
+    BB<W> pl[RP_COUNT];
+    {
+        const uint64_t* g = rt.planes + (size_t)q * RP_COUNT * W;
+#pragma unroll
+        for (int k = 0; k < (int)RP_COUNT; ++k) pl[k] = BB<W>::load(g + k * W);
+    }
     const uint4 inf = p.tab.info[q];
     const uint32_t X = inf.x & 0xFFu, Y = (inf.x >> 8) & 0xFFu;
     const uint32_t tx = inf.y & 0xFFu, ty = (inf.y >> 8) & 0xFFu;
     const uint32_t P = p.pitch;
-    const BB<W> cells = BB<W>::load(pl + RP_CELLS * W);
-    const BB<W> lattice = BB<W>::load(pl + RP_LATTICE * W);
-    const BB<W> gaps = BB<W>::load(pl + RP_GAPS * W);
-    const BB<W> nfirst = BB<W>::load(pl + RP_NOTFIRST * W), nlast = BB<W>::load(pl + RP_NOTLAST * W);
+    const BB<W> cells = pl[RP_CELLS];
+    const BB<W> lattice = pl[RP_LATTICE];
+    const BB<W> gaps = pl[RP_GAPS];
+    const BB<W> nfirst = pl[RP_NOTFIRST], nlast = pl[RP_NOTLAST];
     const BB<W> allowed = lattice.andnot(gaps | vis) | cells;
     const uint32_t ir = rt.inst_range[q];
     const FitIn fin{&rt, ir & 0xFFFFu, ir >> 16, (X - 1) / 2, (Y - 1) / 2};
@@ -263,20 +296,21 @@ __device__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const BB<W>& vi
             }
         }
         // squares: at most one non-zero colour (533-551)
-        const BB<W> sq = Rc & BB<W>::load(pl + RP_SQUARE * W);
+        const BB<W> sq = Rc & pl[RP_SQUARE];
         if (sq.any()) {
             int ncol = 0;
-            for (int c = 0; c < 8; ++c) ncol += (sq & BB<W>::load(pl + (RP_COL1 + c) * W)).any();
+#pragma unroll
+            for (int c = 0; c < 8; ++c) ncol += (sq & pl[RP_COL1 + c]).any();
             sq_ok &= ncol <= 1;
         }
         // stars (553-619)
-        const BB<W> st = Rc & BB<W>::load(pl + RP_STAR * W);
+        const BB<W> st = Rc & pl[RP_STAR];
         if (st.any()) {
-            star_ok &= !st.andnot(BB<W>::load(pl + RP_COLORED * W)).any();
-            const BB<W> m0 = BB<W>::load(pl + RP_M0 * W), m1 = BB<W>::load(pl + RP_M1 * W),
-                        m2 = BB<W>::load(pl + RP_M2 * W);
+            star_ok &= !st.andnot(pl[RP_COLORED]).any();
+            const BB<W> m0 = pl[RP_M0], m1 = pl[RP_M1], m2 = pl[RP_M2];
+#pragma unroll
             for (int c = 0; c < 8; ++c) {
-                const BB<W> col = Rc & BB<W>::load(pl + (RP_COL1 + c) * W);
+                const BB<W> col = Rc & pl[RP_COL1 + c];
                 if (!(st & col).any()) continue;
                 const int tot = (col & m0).popc() + 2 * (col & m1).popc() + 4 * (col & m2).popc();
                 star_ok &= tot == 2;
@@ -285,6 +319,7 @@ __device__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const BB<W>& vi
         // poly / ylop (648-709)
         int pa = 0, ya = 0;
         bool has = false;
+        if ((Rc & pl[RP_INST]).any())                          // regions without instances skip the list
         for (uint32_t k = 0; k < fin.count; ++k) {
             const uint32_t e = rt.inst[fin.first + k];
             if (!Rc.test(e & 0x3FFu)) continue;
@@ -294,7 +329,9 @@ __device__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const BB<W>& vi
         }
         if (has) {
             bool ok = Rc.popc() == pa - ya;
+#ifndef SPARC_DIAG_RULES_NO_FIT
             if (ok) ok = exact_fit<W>(fin, Rc, P, p.err);
+#endif
             if (ok) fit_ok |= 1ull << (rid & 63);
             poly_ok &= ok;
         }
@@ -304,13 +341,11 @@ __device__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const BB<W>& vi
     const BB<W> a = vis.shr(P), b = vis.shl(P), c = vis.shr(1), d = vis.shl(1);
     const BB<W> s1 = a ^ b, c1 = a & b, s2 = c ^ d, c2 = c & d;
     const BB<W> n0 = s1 ^ s2, k0 = s1 & s2, n1 = c1 ^ c2 ^ k0, n2 = c1 & c2;
-    const BB<W> bad = BB<W>::load(pl + RP_TRI * W) &
-                      ((n0 ^ BB<W>::load(pl + RP_TRI0 * W)) | (n1 ^ BB<W>::load(pl + RP_TRI1 * W)) |
-                       (n2 ^ BB<W>::load(pl + RP_TRI2 * W)));
+    const BB<W> bad = pl[RP_TRI] & ((n0 ^ pl[RP_TRI0]) | (n1 ^ pl[RP_TRI1]) | (n2 ^ pl[RP_TRI2]));
     const bool tri_ok = !bad.any();
     const bool reached = x == tx && y == ty;
     const bool gap_ok = !(gaps & vis).any();
-    const bool dot_ok = !BB<W>::load(pl + RP_DOTS * W).andnot(vis).any();
+    const bool dot_ok = !pl[RP_DOTS].andnot(vis).any();
     uint32_t bits = (uint32_t)reached | 2u | ((uint32_t)gap_ok << 2) | ((uint32_t)dot_ok << 3) |
                     ((uint32_t)sq_ok << 4) | ((uint32_t)star_ok << 5) | ((uint32_t)tri_ok << 6) |
                     ((uint32_t)poly_ok << 7);

@@ -281,10 +281,10 @@ def pack_table(puzzles, pitch=None, words=None):
 
 
 # ----------------------------------------------------------------------------------- rule audit
-RULE_PLANES = 24   # SPARC_RULE_PLANES
+RULE_PLANES = 25   # SPARC_RULE_PLANES
 (RP_CELLS, RP_LATTICE, RP_GAPS, RP_DOTS, RP_TRI, RP_TRI0, RP_TRI1, RP_TRI2, RP_STAR, RP_SQUARE,
  RP_COLORED) = range(11)
-RP_COL1, RP_M0, RP_M1, RP_M2, RP_NOTFIRST, RP_NOTLAST = 11, 19, 20, 21, 22, 23
+RP_COL1, RP_M0, RP_M1, RP_M2, RP_NOTFIRST, RP_NOTLAST, RP_INST = 11, 19, 20, 21, 22, 23, 24
 RULE_SKIP_LAYERS = ("visited", "gaps", "agent_location", "target_location")   # SPaRC_Gym.py:466
 
 
@@ -389,6 +389,7 @@ def pack_rules(puzzles, table: PuzzleTable) -> RulesTable:
                         shape_ids[key] = len(shapes)
                         shapes.append(key)
                     b = x * pitch + y
+                    planes[q, RP_INST, b >> 6] |= np.uint64(1) << np.uint64(b & 63)
                     inst.append(b | (int(ylop) << 10) | (((x - 1) // 2) << 11) | (((y - 1) // 2) << 14)
                                 | (shape_ids[key] << 17))
         if len(inst) - first > 0xFFFF or first > 0xFFFF:

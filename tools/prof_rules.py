@@ -9,6 +9,9 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "sparc-gym_amd"))
 
+if "--lib" in sys.argv:   # a diagnostic build of the library (set before the package loads it)
+    os.environ["SPARC_DIAG_LIB"] = os.path.abspath(sys.argv[sys.argv.index("--lib") + 1])
+
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
@@ -22,6 +25,7 @@ ap.add_argument("--envs", type=int, default=65536)
 ap.add_argument("--warm", type=int, default=20)
 ap.add_argument("--launches", type=int, default=10)
 ap.add_argument("--rule-pool", action="store_true", help="rule-consistent puzzles instead of the bench pool")
+ap.add_argument("--lib", default=None, help="path of a diagnostic build of libsparc_gym_amd.so")
 a = ap.parse_args()
 sizes, full, tb = bench.CONFIGS[a.config]
 recs = (synthetic.make_rule_puzzles(1024, seed=0, sizes=sizes) if a.rule_pool
