@@ -493,19 +493,20 @@ struct Env<1, TB, Stack> {
     const uint8_t* diag_lds = nullptr;
 #endif
 
-    // _load_puzzle (SPaRC_Gym.py:166-187) with fresh planes; step0 = -1 inside a rollout (the
-    // same step's counter increment brings it to 0).  Inside a rollout the step that resets
-    // recomputes pending, outcome and legal itself, and rl is unused until the first move.
+    // _load_puzzle (SPaRC_Gym.py:166-187) with fresh planes: the puzzle rows and the board,
+    // not the trie state (inside a rollout the done step's phase_trie runs after this).  The
+    // step that resets recomputes pending, outcome and legal itself, and rl is unused until
+    // the first move.
     template <class Src>
     __device__ __forceinline__ void reset_rows(const Src& src, uint32_t q) {
         pid = q;
         e = load_puzzle(src, q);
         fr = src.get_init(q);
-        off = ((pflags >> 1) & 1u) ^ 1u;
     }
     template <class Src>
     __device__ __forceinline__ void reset(const Params& p, const Src& src, uint32_t q) {
         reset_rows(src, q);
+        off = ((pflags >> 1) & 1u) ^ 1u;
         len = 1;
         nn = ((pflags >> 3) & 1u) << 15;   // node 0 (the root); it is a solution iff [start] is one
         step = 0;
@@ -526,8 +527,9 @@ struct Env<1, TB, Stack> {
 
     // gymnasium next-step autoreset (reset(), SPaRC_Gym.py:1087): the step after a done step
     // loads the next puzzle (index + 1 mod P), ignores its action and returns reward 0, flag
-    // 64.  Only the puzzle rows, the board and the counters are set here; the trie state is
-    // set to the root by that step's phase_trie (the done step's phase_trie still needs it).
+    // 64.  Only the puzzle rows, the board and the counters are set here; the trie state (nn,
+    // off) is set to the root by that step's phase_trie: in k_rollout1 the done step's
+    // phase_trie runs after this call and still needs it.
     template <class Src>
     __device__ __forceinline__ void reset_next(const Params& p, const Src& src) {
         if (pending & (uint32_t)(p.autoreset == 1)) {

@@ -262,3 +262,60 @@ def test_device_reset_rejects_bad_index(on_gpu):
     v.core.reset_device(q.data_ptr())
     with pytest.raises(ValueError):
         v.core.sync()
+
+
+@pytest.mark.parametrize("n", [2624, 3000])
+def test_w1_chunked_partial_workgroups(on_gpu, n):
+    """k_rollout1 (W = 1): full workgroups through the I/O wave next to a partial last workgroup
+    (n = 2624: n % 16 == 0, tiled) or every workgroup on the direct path (n = 3000: untiled);
+    launches of 100 + 57 + 1 + 32 steps (tails, single steps, exact tiles) equal one launch of
+    190 steps, reward codes, flags and per-env stats alike, and equal the oracle."""
+    from sparc_gym_amd import SPaRCVecEnv
+    proc, table = _make("7x7_full", seed=9)
+    assert table.words == 1
+    pids = (np.arange(n) * 7) % len(proc)
+    acts = torch.randint(0, 5, (190, n), dtype=torch.uint8, device="cuda")
+    kw = dict(processed=proc, table=table, traceback=True, observation="compact", max_steps=60)
+    a = SPaRCVecEnv(n, **kw)
+    a.reset(options={"puzzle_index": pids})
+    sa = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
+    full = a.rollout(190, acts, stats=sa)
+    b = SPaRCVecEnv(n, **kw)
+    b.reset(options={"puzzle_index": pids})
+    sb = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
+    parts, t = [], 0
+    for T in (100, 57, 1, 32):
+        parts.append(b.rollout(T, acts[t:t + T].contiguous(), stats=sb))
+        t += T
+    for key in ("reward_code", "flags"):
+        assert torch.equal(full[key], torch.cat([p[key] for p in parts]))
+    assert torch.equal(sa, sb)
+    o = COracle(oracle_pool_from_processed(proc), n, True, 60, autoreset=1)
+    o.reset(pids)
+    ost = np.zeros((n, 4), np.int32)
+    ro, fo = o.rollout(190, acts.cpu().numpy(), stats=ost)
+    assert np.array_equal(full["reward_code"].cpu().numpy(), ro)
+    assert np.array_equal(full["flags"].cpu().numpy(), fo)
+    assert np.array_equal(sa.cpu().numpy(), ost)
+    _assert_states_equal(b.state(), o.state(), table)
+
+
+def test_w1_rollout_without_outputs_keeps_state_and_stats(on_gpu):
+    """record=False (no reward / flag tensors) and in-kernel random actions: same state and
+    stats as the recorded run."""
+    from sparc_gym_amd import SPaRCVecEnv
+    proc, table = _make("7x7_full", seed=10)
+    n = 4096
+    pids = np.arange(n) % len(proc)
+    kw = dict(processed=proc, table=table, traceback=True, observation="compact")
+    runs = []
+    for record in (True, False):
+        v = SPaRCVecEnv(n, **kw)
+        v.reset(options={"puzzle_index": pids})
+        st = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
+        v.rollout(96, None, seed=3, stats=st, record=record)
+        runs.append((st.cpu().numpy(), v.state()))
+    assert np.array_equal(runs[0][0], runs[1][0])
+    for k in ("x", "y", "step", "path_len", "puzzle", "outcome", "pending"):
+        assert np.array_equal(runs[0][1][k], runs[1][1][k]), k
+    assert np.array_equal(runs[0][1]["visited"], runs[1][1]["visited"])
