@@ -319,3 +319,31 @@ def test_w1_rollout_without_outputs_keeps_state_and_stats(on_gpu):
     for k in ("x", "y", "step", "path_len", "puzzle", "outcome", "pending"):
         assert np.array_equal(runs[0][1][k], runs[1][1][k]), k
     assert np.array_equal(runs[0][1]["visited"], runs[1][1]["visited"])
+
+
+@pytest.mark.parametrize("max_steps", [3, 9, 25])
+def test_many_short_episodes_vs_oracle(on_gpu, max_steps):
+    """Thousands of autoresets per launch (short max_steps, puzzles with many solutions sharing
+    prefixes, mostly-legal actions): every done step's reward and the step after it are where
+    the pipelined rollout hands the trie state over to the reset, so compare them all."""
+    from sparc_gym_amd import SPaRCVecEnv
+    recs = synthetic.make_puzzles(256, seed=max_steps, sizes=((3, 3),), n_solutions=8,
+                                  shared_prefix_prob=0.9, full_properties=False)
+    proc = process_puzzles(recs)
+    table = pack_table(proc)
+    n, T = 16384, 240
+    rng = np.random.default_rng(max_steps)
+    pids = rng.integers(len(proc), size=n)
+    acts = rng.integers(0, 4, size=(T, n)).astype(np.uint8)
+    v = SPaRCVecEnv(n, processed=proc, table=table, traceback=True, max_steps=max_steps, observation="compact")
+    v.reset(options={"puzzle_index": pids})
+    st = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
+    out = v.rollout(T, torch.from_numpy(acts).cuda(), stats=st)
+    o = COracle(oracle_pool_from_processed(proc), n, True, max_steps, autoreset=1)
+    o.reset(pids)
+    ost = np.zeros((n, 4), np.int32)
+    ro, fo = o.rollout(T, acts, stats=ost)
+    r = out["reward_code"].cpu().numpy()
+    assert np.array_equal(r, ro) and np.array_equal(out["flags"].cpu().numpy(), fo)
+    assert np.array_equal(st.cpu().numpy(), ost)
+    assert (r == 100).sum() > 100        # the case needs solved episodes, and many of them
