@@ -64,7 +64,7 @@ __global__ void __launch_bounds__(256) kern(uint64_t* out, uint32_t seed) {
     }
     const uint64_t t1 = __builtin_amdgcn_s_memtime();
     if (threadIdx.x == 0) out[blockIdx.x] = t1 - t0;
-    if (a == 0x12345678u && b == 1u && c == 2u && x == 3u && y == 4u) out[blockIdx.x + 4096] = a + b + c + d;
+    if (a == 0x12345678u && b == 1u && c == 2u && x == 3u && y == 4u) out[blockIdx.x + 8192] = a + b + c + d;
 }
 
 template <int K>
@@ -80,7 +80,7 @@ double run(uint64_t* d, int blocks, int instr_per_iter) {
 
 int main() {
     uint64_t* d;
-    (void)hipMalloc(&d, 8 * 8192);
+    (void)hipMalloc(&d, 8 * 16384);
     const int blocks = 256;   // 1 workgroup of 4 waves per CU: one wave per SIMD
     const char* names2[] = {"ds_write_b8 1/dword", "ds_write_b32", "v_cmp->s_or->s_or->s_or", "valu-only bool", "v_cmp,v_cmp,s_and,s_and"};
     const char* names[] = {"valu u32 indep", "valu u32 dep chain", "v_lsh*_b64 indep", "v_cmp->v_cndmask dep",
@@ -100,5 +100,13 @@ int main() {
         r2[3] = run<15>(d, blocks, 256); r2[4] = run<16>(d, blocks, 256);
     }
     for (int k = 0; k < 5; ++k) printf("%-28s %8.3f ticks/instr\n", names2[k], r2[k]);
+    // two waves per SIMD (two workgroups per CU): per-wave ticks per instruction
+    double r3[4];
+    for (int pass = 0; pass < 2; ++pass) {
+        r3[0] = run<0>(d, 2 * blocks, 256); r3[1] = run<1>(d, 2 * blocks, 256);
+        r3[2] = run<2>(d, 2 * blocks, 256); r3[3] = run<6>(d, 2 * blocks, 256);
+    }
+    printf("2 waves/SIMD: valu indep %.3f, valu dep %.3f, b64 shifts %.3f, ds_write_b8 %.3f ticks/instr/wave\n",
+           r3[0], r3[1], r3[2], r3[3]);
     return 0;
 }
