@@ -31,11 +31,13 @@ sys.path.insert(0, os.path.join(REPO, "sparc-gym_amd"))
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
 CONFIGS = {
-    # name: (grid sizes, full property set, traceback)
-    "c2": (((3, 3),), False, False),
-    "c3": (((3, 3),), True, True),
-    "c4": (((2, 2), (3, 3), (4, 4), (5, 5)), True, True),
+    # name: (grid sizes, full property set, traceback, 'new' observation planes every step)
+    "c2": (((3, 3),), False, False, False),
+    "c3": (((3, 3),), True, True, False),
+    # BASELINE configs[3]: 262,144 mixed 5x5-11x11 puzzles, observation='new' dict pack
+    "c4": (((2, 2), (3, 3), (4, 4), (5, 5)), True, True, True),
 }
+DEFAULT_ENVS = {"c2": 4096, "c3": 65536, "c4": 262144}
 
 
 def parse():
@@ -43,9 +45,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=200)
-    ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--envs", type=int, default=0, help="envs per GPU (0 = the config's: c2 4,096, c3 65,536, "
+                                                         "c4 262,144)")
     ap.add_argument("--chunk", type=int, default=0,
-                    help="env-steps per rollout launch (0 = all timed steps in one launch)")
+                    help="env-steps per rollout launch (0 = all timed steps in one launch; with observation "
+                         "traces (c4) 0 = 50)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--mode", default="rollout", choices=["rollout", "step"])
@@ -62,8 +66,9 @@ def state_bytes_per_env(words, traceback):
     return 8 * words + (16 * words if traceback else 0) + 16
 
 
-def cpu_baseline(proc, tb, max_steps, seconds):
-    """C oracle (sparc_oracle.c, 1 thread) on a bounded sample of the same workload."""
+def cpu_baseline(proc, tb, max_steps, seconds, obs_dims=None):
+    """C oracle (sparc_oracle.c, 1 thread) on a bounded sample of the same workload (with
+    obs_dims = (x_dim, y_dim): also writing the 'new' observation planes of every step)."""
     from oracle import COracle
     pool = [{"x_size": p["x_size"], "y_size": p["y_size"], "start": list(p["start_location"]),
              "target": list(p["target_location"]), "solution_count": p["solution_count"],
@@ -74,7 +79,10 @@ def cpu_baseline(proc, tb, max_steps, seconds):
     steps, T = 0, 64
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
-        o.rollout(T, None, seed=1, t0=steps)
+        if obs_dims:
+            o.rollout_obs(T, obs_dims[0], obs_dims[1], None, seed=1, t0=steps)
+        else:
+            o.rollout(T, None, seed=1, t0=steps)
         steps += T
     dt = time.perf_counter() - t0
     c_rate = n * steps / dt
@@ -92,6 +100,7 @@ def cpu_baseline(proc, tb, max_steps, seconds):
     py_rate = k / (time.perf_counter() - t1)
     return {"value": round(c_rate, 1), "unit": "env-steps/s", "cores": 1, "kind": "port",
             "sample": f"oracle/sparc_oracle.c, {n} envs x {steps} steps, random actions, next-step autoreset, "
+                      f"{'visited + agent_location planes written every step, ' if obs_dims else ''}"
                       f"1 thread, {dt:.1f} s; CPU {platform.processor() or platform.machine()}, "
                       f"os.cpu_count()={os.cpu_count()}",
             "python_port_value": round(py_rate, 1),
@@ -125,7 +134,9 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    sizes, full, tb = CONFIGS[args.config]
+    sizes, full, tb, obs = CONFIGS[args.config]
+    if args.envs <= 0:
+        args.envs = DEFAULT_ENVS[args.config]
     recs = synthetic.make_puzzles(args.puzzles, seed=0, sizes=sizes, full_properties=full)
     proc = process_puzzles(recs)
     table = pack_table(proc)
@@ -136,7 +147,17 @@ def main():
     vec.reset(options={"puzzle_index": (gid * 2654435761 % len(proc)).astype(np.int64)})
 
     K, W = args.steps, args.warmup
-    chunk = K if args.chunk <= 0 else max(1, min(args.chunk, K))
+    if args.chunk <= 0:
+        args.chunk = 50 if obs else K
+    chunk = max(1, min(args.chunk, K))
+    # observation traces [chunk, N, x_dim, y_dim] int32 (visited, agent_location), reused by
+    # every launch (one launch = one chunk of steps; a consumer reads them between launches)
+    X, Y = vec.x_dim, vec.y_dim
+    plane_bytes = X * Y * 4
+    ovis = oag = None
+    if obs:
+        ovis = torch.empty((chunk, n, X, Y), dtype=torch.int32, device=dev)
+        oag = torch.empty_like(ovis)
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
     actions = torch.randint(0, 4, (K, n), dtype=torch.uint8, device=dev, generator=g)
@@ -160,7 +181,11 @@ def main():
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if events is not None else None
                 if ev:
                     ev[0].record(stream)
-                core.rollout_device(c, ap + t * n, rp + t * n, fp + t * n, s_ptr)
+                if obs:
+                    core.rollout_obs_device(c, ap + t * n, rp + t * n, fp + t * n, s_ptr, ovis.data_ptr(),
+                                            oag.data_ptr(), X, Y)
+                else:
+                    core.rollout_device(c, ap + t * n, rp + t * n, fp + t * n, s_ptr)
                 if ev:
                     ev[1].record(stream)
                     events.append((ev, c))
@@ -206,9 +231,10 @@ def main():
     # launch the state (load + store) and, for rollouts, the stats record (load + store)
     sb = state_bytes_per_env(table.words, tb)
     per_env_launch = 2 * sb + (32 if args.mode == "rollout" else 0)
-    bytes_launch = n * (3 * avg_T + per_env_launch)
+    per_step = 3 + (2 * plane_bytes if obs and args.mode == "rollout" else 0)
+    bytes_launch = n * (per_step * avg_T + per_env_launch)
     achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
-    kernel = ("k_rollout1" if table.words == 1 else "k_rollout") if args.mode == "rollout" else "k_step"
+    kernel = ("k_rollout1" if table.words == 1 and not obs else "k_rollout") if args.mode == "rollout" else "k_step"
     workload = f"{args.config}_{args.mode}_n{n}_chunk{chunk if args.mode == 'rollout' else 1}"
     traffic = load_traffic(workload, kernel)
     out = {
@@ -226,7 +252,9 @@ def main():
         "data": "synthetic SPaRC-schema puzzles (sparc_gym_amd.synthetic, seed 0); uniform random actions in HBM",
         "config": {"workload": f"{args.config}: {n} envs/GPU, lattices {['%dx%d' % (2*w+1, 2*h+1) for w, h in sizes]}, "
                                f"{'full property set' if full else 'base planes'}, traceback={tb}, "
-                               f"max_steps={args.max_steps}, next-step autoreset, {args.puzzles} puzzles",
+                               f"max_steps={args.max_steps}, next-step autoreset, {args.puzzles} puzzles"
+                               + (f", observation='new': visited + agent_location int32 planes "
+                                  f"[N, {X}, {Y}] written every step" if obs else ""),
                    "mode": args.mode, "envs_per_gpu": n, "env_steps_per_launch": chunk if args.mode == "rollout" else 1,
                    "parallelism": f"dp{world} (env shards, {'RCCL' if args.backend == 'nccl' else args.backend} "
                                   f"all_gather of per-env stats at end of batch)"},
@@ -234,13 +262,15 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                      "kernel": kernel, "kernel_avg_ms": round(avg_ms, 4), "launches": len(kern_ms),
                      "algorithmic_bytes_per_launch": int(bytes_launch),
-                     "bytes_model": f"per env-step 3 B (action, reward code, flags); per env per launch "
+                     "bytes_model": f"per env-step {per_step} B (action, reward code, flags"
+                                    f"{f', visited + agent_location planes 2 x {plane_bytes} B' if obs else ''}"
+                                    f"); per env per launch "
                                     f"{per_env_launch} B (state {sb} B load+store"
                                     f"{', stats 16 B load+store' if args.mode == 'rollout' else ''})"},
         "episodes": summary,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb = cpu_baseline(proc, tb, args.max_steps, args.cpu_seconds)
+        cb = cpu_baseline(proc, tb, args.max_steps, args.cpu_seconds, (X, Y) if obs else None)
         out["cpu_baseline"] = cb
         out["gpu_vs_cpu"] = round(value / cb["value"], 1)
     elif rank == 0:

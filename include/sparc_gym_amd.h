@@ -151,6 +151,25 @@ int sparc_rollout_device(void *ctx, int32_t T, const uint8_t *d_actions, uint64_
  * NULL).  The reference returns these planes by reference every step (SPaRC_Gym.py:979). */
 int sparc_obs_pack_device(void *ctx, int32_t *d_visited, int32_t *d_agent, int32_t x_dim, int32_t y_dim);
 
+/* step (SPaRC_Gym.py:1111-1238) and the 'new' observation it returns (_get_obs 956-979) in ONE
+ * launch: reward/flags as sparc_step_device, then the post-step visited / agent_location
+ * planes [N][x_dim][y_dim] int32 (either may be NULL), the current puzzle index [N] (after any
+ * autoreset; may be NULL) and the agent location [N] = x | y << 8 (may be NULL).
+ * x_dim * y_dim <= 256.  Device pointers, asynchronous. */
+int sparc_step_obs_device(void *ctx, const uint8_t *d_actions, int8_t *d_reward, uint8_t *d_flags,
+                          int32_t *d_visited, int32_t *d_agent, int32_t x_dim, int32_t y_dim,
+                          uint32_t *d_puzzle, uint32_t *d_xy);
+
+/* sparc_rollout_device that also records the 'new' observation after every step: planes
+ * [T][N][x_dim][y_dim] int32 (visited / agent_location; either may be NULL), so step t's
+ * entries equal sparc_step_obs_device's after the t-th of T single steps.  Every store is a
+ * whole 16-B piece of a contiguous per-wave run when N * x_dim * y_dim % 4 == 0 and the
+ * pointers are 16-B aligned.  x_dim * y_dim <= 256.  This mode is HBM-write-bound
+ * (8 * x_dim * y_dim bytes per env-step). */
+int sparc_rollout_obs_device(void *ctx, int32_t T, const uint8_t *d_actions, uint64_t seed, uint64_t t0,
+                             int8_t *d_reward, uint8_t *d_flags, int32_t *d_stats, int32_t *d_visited,
+                             int32_t *d_agent, int32_t x_dim, int32_t y_dim);
+
 int sparc_read_state(void *ctx, const sparc_state_host *out);
 /* device-to-device copy of one SoA state array (`which` as in sparc_state_ptr) into d_out,
  * ordered on the context's stream (e.g. the per-env puzzle index after autoresets). */

@@ -135,6 +135,26 @@ uint32_t oracle_rand_action(uint64_t seed, uint64_t env, uint64_t t) {
 int oracle_rollout(const oracle_pool *pool, int n, oracle_env *envs, int T, const uint8_t *actions,
                    uint64_t seed, uint64_t env_offset, uint64_t t0, int traceback, int max_steps,
                    int autoreset, int8_t *rew, uint8_t *flags, int32_t *stats) {
+    return oracle_rollout_obs(pool, n, envs, T, actions, seed, env_offset, t0, traceback, max_steps, autoreset,
+                              rew, flags, stats, NULL, NULL, 0, 0);
+}
+
+/* obs['base']['visited'] / ['agent_location'] of env e as int32 planes [xd][yd] (_get_obs,
+ * SPaRC_Gym.py:956-979; zero outside the puzzle's lattice) */
+static void write_planes(const oracle_env *e, int32_t *vis, int32_t *agent, int xd, int yd) {
+    for (int x = 0; x < xd; ++x)
+        for (int y = 0; y < yd; ++y) {
+            int inb = x < ORACLE_MAXDIM && y < ORACLE_MAXDIM;
+            if (vis) vis[x * yd + y] = inb ? e->visited[x][y] : 0;
+            if (agent) agent[x * yd + y] = (x == e->x && y == e->y);
+        }
+}
+
+int oracle_rollout_obs(const oracle_pool *pool, int n, oracle_env *envs, int T, const uint8_t *actions,
+                       uint64_t seed, uint64_t env_offset, uint64_t t0, int traceback, int max_steps,
+                       int autoreset, int8_t *rew, uint8_t *flags, int32_t *stats, int32_t *vis,
+                       int32_t *agent, int xd, int yd) {
+    const size_t plane = (size_t)xd * yd;
     for (int i = 0; i < n; ++i) {
         oracle_env *e = &envs[i];
         for (int t = 0; t < T; ++t) {
@@ -157,6 +177,9 @@ int oracle_rollout(const oracle_pool *pool, int n, oracle_env *envs, int T, cons
             }
             if (rew) rew[(size_t)t * n + i] = c;
             if (flags) flags[(size_t)t * n + i] = f;
+            if (vis || agent)
+                write_planes(e, vis ? vis + ((size_t)t * n + i) * plane : NULL,
+                             agent ? agent + ((size_t)t * n + i) * plane : NULL, xd, yd);
         }
     }
     return 0;

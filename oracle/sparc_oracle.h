@@ -56,6 +56,12 @@ int oracle_step(const oracle_pool *pool, oracle_env *e, int action, int tracebac
 int oracle_rollout(const oracle_pool *pool, int n, oracle_env *envs, int T, const uint8_t *actions,
                    uint64_t seed, uint64_t env_offset, uint64_t t0, int traceback, int max_steps,
                    int autoreset, int8_t *rew, uint8_t *flags, int32_t *stats);
+/* oracle_rollout that also records the post-step visited / agent_location planes of every
+ * step: [T][n][xd][yd] int32 (either may be NULL) */
+int oracle_rollout_obs(const oracle_pool *pool, int n, oracle_env *envs, int T, const uint8_t *actions,
+                       uint64_t seed, uint64_t env_offset, uint64_t t0, int traceback, int max_steps,
+                       int autoreset, int8_t *rew, uint8_t *flags, int32_t *stats, int32_t *vis,
+                       int32_t *agent, int xd, int yd);
 uint32_t oracle_rand_action(uint64_t seed, uint64_t env, uint64_t t);
 #ifdef __cplusplus
 }

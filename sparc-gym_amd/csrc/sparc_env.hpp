@@ -306,6 +306,15 @@ struct Env {
         return code;
     }
 
+    // obs['base']['visited'] bits and the agent's bit index (SPaRC_Gym.py:956-979)
+    template <class Src>
+    __device__ __forceinline__ void obs_words(const Params& p, const Src&, uint64_t (&v)[W], uint32_t& ab) const {
+#pragma unroll
+        for (int k = 0; k < W; ++k) v[k] = vis[k];
+        ab = x * p.pitch + y;
+    }
+    __device__ __forceinline__ uint32_t agent_xy(const Params&) const { return x | (y << 8); }
+
     // ---- SoA <-> registers
     template <class Src>
     __device__ __forceinline__ void load(const Params& p, const Src& src, uint32_t i) {
@@ -628,6 +637,18 @@ struct Env<1, TB, Stack> {
         const bool match = (off == 0) & (nn >= 0x8000u);
         code = pending ? (match ? 100 : (outcome != 1 ? -100 : 0)) : 0;
         sol = (uint32_t)(pending & match);
+    }
+
+    // obs['base']['visited'] bits (visited = in the puzzle and not free, plus the start, as
+    // store() writes them) and the agent's bit index
+    template <class Src>
+    __device__ __forceinline__ void obs_words(const Params& p, const Src& src, uint64_t (&v)[1], uint32_t& ab) const {
+        v[0] = ((src.get_init(pid) & ~fr) >> p.pitch) | (1ull << (src.get_row1(pid).x & 0xFFu));
+        ab = e;
+    }
+    __device__ __forceinline__ uint32_t agent_xy(const Params& p) const {
+        const uint32_t x = e / p.pitch;
+        return x | ((e - x * p.pitch) << 8);
     }
 
     template <class Src>

@@ -102,6 +102,129 @@ __device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_wave_barrier();
 }
 
+// ---------------------------------------------------------------------------------------------
+// 'new' observation planes, obs['base']['visited'] and obs['base']['agent_location']
+// (SPaRC_Gym.py:956-979; int32 [x][y] planes), written by one wave for its 64 envs.
+//
+// Layout [...][N][XD][YD] int32, the lattice padded to XD x YD (the pool's largest).  A wave's
+// envs own one contiguous run of 64 * XD * YD entries per plane, so instead of each lane
+// writing its own env's plane (64 scattered rows per store instruction) every lane stages its
+// board and agent bit in LDS and the wave then writes the run in 16-B pieces: piece j holds
+// entries 4j..4j+3, whichever env they belong to, and one store instruction covers 1 KB of
+// contiguous memory.  A LUT maps plane cell x*YD + y to board bit x*pitch + y (0xFFFF when
+// the cell is outside the board).
+constexpr uint32_t kObsCells = 256;   // XD * YD limit
+constexpr uint16_t kObsNone = 0xFFFFu;
+template <int W>
+struct ObsWave {
+    uint32_t vis[2 * W][64];   // visited board in 32-bit halves, half-major
+    uint32_t ab[64];           // agent bit index (kObsNone for lanes without an env)
+};
+template <int W>
+__host__ __device__ constexpr size_t obs_lds_bytes() { return kWaves * sizeof(ObsWave<W>) + kObsCells * sizeof(uint16_t); }
+
+__device__ __forceinline__ void obs_build_lut(uint16_t* lut, uint32_t XD, uint32_t YD, uint32_t pitch, uint32_t W,
+                                              uint32_t tid, uint32_t nthreads) {
+    for (uint32_t c = tid; c < kObsCells; c += nthreads) {
+        const uint32_t x = c / YD, y = c - x * YD, b = x * pitch + y;
+        lut[c] = (c < XD * YD && y < pitch && b < 64u * W) ? (uint16_t)b : kObsNone;
+    }
+}
+
+// the wave's envs [0, cnt) -> planes at vout / aout (run starts, entry `base` of the whole
+// array, for the alignment test); every lane of the wave must call this (wave-uniform)
+template <int W>
+__device__ __forceinline__ void obs_emit(ObsWave<W>* ow, const uint16_t* lut, uint32_t lane, bool has_env,
+                                         const uint64_t (&v)[W], uint32_t ab, uint32_t cnt, uint32_t XY,
+                                         int32_t* __restrict__ vout, int32_t* __restrict__ aout) {
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+        ow->vis[2 * k][lane] = (uint32_t)v[k];
+        ow->vis[2 * k + 1][lane] = (uint32_t)(v[k] >> 32);
+    }
+    ow->ab[lane] = has_env ? ab : (uint32_t)kObsNone;
+    wave_lds_fence();
+    const uint32_t total = cnt * XY;
+    // 16-B stores need both runs 16-B aligned (true whenever N * XY % 4 == 0)
+    const bool vec = (((reinterpret_cast<uintptr_t>(vout) | reinterpret_cast<uintptr_t>(aout)) & 15u) == 0);
+    uint32_t f = 4u * lane;                       // first entry of this lane's piece
+    uint32_t l = f / XY, c = f - l * XY;          // its env and cell
+    const uint32_t dl = 256u / XY, dc = 256u - dl * XY;   // a 64-piece stride in envs / cells
+    for (; f < total; f += 256u) {
+        uint32_t vv[4], aa[4];
+        uint32_t ll = l, cc = c;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t b = lut[cc];
+            const uint32_t word = ow->vis[(b >> 5) & (2 * W - 1)][ll & 63u];
+            vv[k] = b == kObsNone ? 0u : (word >> (b & 31u)) & 1u;
+            aa[k] = b == ow->ab[ll & 63u] ? 1u : 0u;
+            ++cc;
+            if (cc == XY) {
+                cc = 0;
+                ++ll;
+            }
+        }
+        if (vec && f + 4u <= total) {
+            if (vout) __builtin_nontemporal_store(u32x4{vv[0], vv[1], vv[2], vv[3]}, reinterpret_cast<u32x4*>(vout + f));
+            if (aout) __builtin_nontemporal_store(u32x4{aa[0], aa[1], aa[2], aa[3]}, reinterpret_cast<u32x4*>(aout + f));
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (f + k < total) {
+                    if (vout) vout[f + k] = (int32_t)vv[k];
+                    if (aout) aout[f + k] = (int32_t)aa[k];
+                }
+            }
+        }
+        c += dc;
+        l += dl;
+        if (c >= XY) {
+            c -= XY;
+            ++l;
+        }
+    }
+    wave_lds_fence();
+}
+
+// step() + the 'new' observation in one launch (SPaRCVecEnv.step): the gym one-call-per-step
+// contract with the planes, the puzzle index and the agent (x | y << 8) of every env
+template <int W, bool TB>
+__global__ void __launch_bounds__(kBlock) k_step_obs(Params p, const uint8_t* __restrict__ act,
+                                                     int8_t* __restrict__ rew, uint8_t* __restrict__ flg,
+                                                     int32_t* __restrict__ vout, int32_t* __restrict__ aout,
+                                                     uint32_t XD, uint32_t YD, uint32_t* __restrict__ pidx,
+                                                     uint32_t* __restrict__ xy) {
+    __shared__ ObsWave<W> ow[kWaves];
+    __shared__ uint16_t lut[kObsCells];
+    obs_build_lut(lut, XD, YD, p.pitch, W, threadIdx.x, kBlock);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x, wave_base = i - lane;
+    if (wave_base >= p.n) return;                 // wave-uniform
+    const bool active = i < p.n;
+    const PuzzleSrc<W> src{p.tab.info, p.tab.root, p.tab.open, p.tab.init, p.tab.row1};
+    Env<W, TB> e;
+    uint64_t v[W];
+#pragma unroll
+    for (int k = 0; k < W; ++k) v[k] = 0;
+    uint32_t ab = 0;
+    if (active) {
+        e.load(p, src, i);
+        uint32_t f;
+        const int c = e.advance(p, src, act[i], f);
+        e.store(p, src, i);
+        rew[i] = (int8_t)c;
+        flg[i] = (uint8_t)f;
+        e.obs_words(p, src, v, ab);
+        if (pidx) pidx[i] = e.pid;
+        if (xy) xy[i] = e.agent_xy(p);
+    }
+    const uint32_t XY = XD * YD, cnt = p.n - wave_base < 64u ? p.n - wave_base : 64u;
+    const size_t run = (size_t)wave_base * XY;
+    obs_emit<W>(&ow[wv], lut, lane, active, v, ab, cnt, XY, vout ? vout + run : nullptr, aout ? aout + run : nullptr);
+}
+
 // T steps per env with the state in VGPRs.  Full waves with `tiled` (16-B aligned I/O, n % 16
 // == 0) move actions / reward codes / flags in [16 steps][64 envs] tiles: one dwordx4 load and
 // two dwordx4 stores per lane per 16 steps, transposed through a per-wave LDS tile, the next
@@ -112,11 +235,19 @@ __device__ __forceinline__ void wave_lds_fence() {
 // EPW = envs per wave: 64, or 32 when the batch gives fewer than two full waves per SIMD (a
 // lone wave issues a VALU op only every ~4 cycles and cannot hide its own trie-record wait;
 // two half-width waves per SIMD fill each other's gaps).
-template <int W, bool TB, bool RAND, bool LDS_TABLE, int EPW>
+// OBS: after every step the wave also writes the 'new' observation planes of step t to
+// vout / aout + t * N * XD * YD (obs_emit; [T][N][XD][YD] int32 traces, either may be NULL).
+struct ObsTrace {
+    int32_t* vout;
+    int32_t* aout;
+    uint32_t XD, YD;
+};
+template <int W, bool TB, bool RAND, bool LDS_TABLE, int EPW, bool OBS = false>
 __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const uint8_t* __restrict__ act,
                                                     uint64_t seed, uint64_t t0, int8_t* __restrict__ rew,
                                                     uint8_t* __restrict__ flg, int4* __restrict__ stats,
-                                                    uint32_t tiled) {
+                                                    uint32_t tiled, ObsTrace ot) {
+    static_assert(!OBS || EPW == 64, "the observation writer needs full 64-lane waves");
     // LDS: [I/O tiles, 3*16*EPW B per wave][W=1 traceback: move stacks, 64*EPW B per wave][rows]
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -124,8 +255,15 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
     uint8_t* tr = ta + EPW * kTile;
     uint8_t* tf = tr + EPW * kTile;
     constexpr size_t kStackOff = tiles_lds_bytes<W, EPW>();
-    constexpr size_t kTableOff = kStackOff + stack_lds_bytes<W, TB, EPW>();
+    constexpr size_t kObsOff = kStackOff + stack_lds_bytes<W, TB, EPW>();
+    constexpr size_t kTableOff = kObsOff + (OBS ? obs_lds_bytes<W>() : 0);
     PuzzleSrc<W> src{p.tab.info, p.tab.root, p.tab.open, p.tab.init, p.tab.row1};
+    ObsWave<W>* ow = reinterpret_cast<ObsWave<W>*>(smem + kObsOff) + wv;
+    const uint16_t* lut = reinterpret_cast<const uint16_t*>(smem + kObsOff + kWaves * sizeof(ObsWave<W>));
+    if constexpr (OBS) {
+        obs_build_lut(const_cast<uint16_t*>(lut), ot.XD, ot.YD, p.pitch, W, threadIdx.x, kBlock);
+        if constexpr (!LDS_TABLE) __syncthreads();
+    }
     if constexpr (LDS_TABLE) {
         const uint32_t P = p.tab.num_puzzles;
         if constexpr (W == 1) {
@@ -167,6 +305,20 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
 #endif
     if (active) e.load(p, src, i);
     int4 acc = make_int4(0, 0, 0, 0);
+    const uint32_t XY = ot.XD * ot.YD;
+    const uint32_t ocnt = p.n - wave_base < (uint32_t)EPW ? p.n - wave_base : (uint32_t)EPW;
+    auto obs = [&](int32_t t) {                      // planes after step t (wave-uniform call)
+        if constexpr (OBS) {
+            uint64_t v[W];
+#pragma unroll
+            for (int k = 0; k < W; ++k) v[k] = 0;
+            uint32_t ab = 0;
+            if (active) e.obs_words(p, src, v, ab);
+            const size_t run = ((size_t)t * n + wave_base) * XY;
+            obs_emit<W>(ow, lut, lane, active, v, ab, ocnt, XY, ot.vout ? ot.vout + run : nullptr,
+                        ot.aout ? ot.aout + run : nullptr);
+        }
+    };
     u32x4 anext = {0u, 0u, 0u, 0u};
     if (!RAND && full && T >= kTile) anext = nt_load16(act + (size_t)r * n + wave_base + c);
 
@@ -187,11 +339,12 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
                     av[j] = RAND ? uint_rand_action(seed, gid, t0 + (uint64_t)(tb + g + j)) : ta[(g + j) * EPW + lane];
-#pragma unroll
+#pragma unroll(OBS ? 1 : 4)
                 for (int j = 0; j < 4; ++j) {
                     const int k = g + j;
                     uint32_t f;
                     const int code = e.advance(p, src, av[j], f);
+                    obs(tb + k);
 #ifndef SPARC_DIAG_NO_OUT_LDS
                     tr[k * EPW + lane] = (uint8_t)code;
                     tf[k * EPW + lane] = (uint8_t)f;
@@ -220,18 +373,21 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
             if (rew) nt_store16(reinterpret_cast<uint8_t*>(rew) + o, *reinterpret_cast<const u32x4*>(tr + r * EPW + c));
             if (flg) nt_store16(flg + o, *reinterpret_cast<const u32x4*>(tf + r * EPW + c));
             wave_lds_fence();
-        } else if (active) {
+        } else if (active || OBS) {
             for (int k = 0; k < cnt; ++k) {
                 const int32_t t = tb + k;
-                const uint32_t a = RAND ? uint_rand_action(seed, gid, t0 + (uint64_t)t) : act[(size_t)t * n + i];
-                uint32_t f;
-                const int code = e.advance(p, src, a, f);
-                if (rew) rew[(size_t)t * n + i] = (int8_t)code;
-                if (flg) flg[(size_t)t * n + i] = (uint8_t)f;
-                acc.x += code;
-                acc.y += (f & 3u) ? 1 : 0;
-                acc.z += ((f & 3u) && code == 100) ? 1 : 0;
-                acc.w += (f & 64u) ? 1 : 0;
+                if (active) {
+                    const uint32_t a = RAND ? uint_rand_action(seed, gid, t0 + (uint64_t)t) : act[(size_t)t * n + i];
+                    uint32_t f;
+                    const int code = e.advance(p, src, a, f);
+                    if (rew) rew[(size_t)t * n + i] = (int8_t)code;
+                    if (flg) flg[(size_t)t * n + i] = (uint8_t)f;
+                    acc.x += code;
+                    acc.y += (f & 3u) ? 1 : 0;
+                    acc.z += ((f & 3u) && code == 100) ? 1 : 0;
+                    acc.w += (f & 64u) ? 1 : 0;
+                }
+                obs(t);
             }
         }
     }
@@ -866,15 +1022,19 @@ int sparc_step_host(void* ctx, const uint8_t* act, int8_t* rew, uint8_t* flags) 
     return sparc_sync(c);
 }
 
-int sparc_rollout_device(void* ctx, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_t t0, int8_t* d_rew,
-                         uint8_t* d_flags, int32_t* d_stats) {
-    Ctx* c = static_cast<Ctx*>(ctx);
+}  // extern "C"
+
+namespace {
+// sparc_rollout_device / sparc_rollout_obs_device; `ot` non-null: observation traces
+int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_t t0, int8_t* d_rew,
+                 uint8_t* d_flags, int32_t* d_stats, const ObsTrace* ot) {
     int rc = check_ctx(c, true);
     if (rc) return rc;
     if (T < 0) return fail(c, SPARC_E_INVALID, "T must be >= 0");
     if (T == 0) return SPARC_OK;
     if ((uint64_t)T * c->n > (1ull << 40)) return fail(c, SPARC_E_INVALID, "T*N too large");
     const Params p = make_params(c);
+    const ObsTrace no_obs{nullptr, nullptr, 1u, 1u};
     int4* st = reinterpret_cast<int4*>(d_stats);
     auto aligned = [](const void* q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & 15u) == 0; };
     const uint32_t tiled = (c->n % 16 == 0) && aligned(d_act) && aligned(d_rew) && aligned(d_flags);
@@ -883,7 +1043,7 @@ int sparc_rollout_device(void* ctx, int32_t T, const uint8_t* d_act, uint64_t se
     // envs per wave: 64.  (Measured on MI355X at 65,536 envs: 32-wide waves, two per SIMD, are
     // 1.3x slower than one full wave per SIMD — a half-empty wave costs the full issue time.)
     const bool half = false;
-    if (c->W == 1) {
+    if (c->W == 1 && !ot) {
         const size_t blocks = (c->n + 255) / 256;
         const size_t per_cu = (blocks + 255) / 256;
         const size_t budget = std::min(kMaxDynLds, (size_t)160 * 1024 / (per_cu ? per_cu : 1));
@@ -913,13 +1073,14 @@ int sparc_rollout_device(void* ctx, int32_t T, const uint8_t* d_act, uint64_t se
     dispatch_w_tb(c->W, c->cfg.traceback, [&](auto w, auto tb) {
         constexpr int W = decltype(w)::value;
         constexpr bool TB = decltype(tb)::value;
-        if constexpr (W == 1) return;   // k_rollout1 above
-        auto go = [&](auto epw_c) {
+        auto go = [&](auto epw_c, auto obs_c) {
             constexpr int EPW = decltype(epw_c)::value;
+            constexpr bool OBS = decltype(obs_c)::value;
+            if constexpr (W == 1 && !OBS) return;   // k_rollout1 above
             const size_t blocks = (c->n + kWaves * EPW - 1) / (kWaves * EPW);
             const size_t per_cu = (blocks + 255) / 256;
             const size_t budget = std::min(kMaxDynLds, (size_t)160 * 1024 / (per_cu ? per_cu : 1));
-            const size_t base = tiles_lds_bytes<W, EPW>() + stack_lds_bytes<W, TB, EPW>();
+            const size_t base = tiles_lds_bytes<W, EPW>() + stack_lds_bytes<W, TB, EPW>() + (OBS ? obs_lds_bytes<W>() : 0);
             const size_t tbytes = table_lds_bytes<W>(c->num_puzzles);
             const bool lds_table = base + tbytes <= budget;
             const size_t shm = base + (lds_table ? tbytes : 0);
@@ -928,18 +1089,61 @@ int sparc_rollout_device(void* ctx, int32_t T, const uint8_t* d_act, uint64_t se
                 if (shm > 64 * 1024)
                     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-                kern<<<g, kBlock, shm, c->stream>>>(p, T, a, seed, t0, d_rew, d_flags, st, tiled);
+                kern<<<g, kBlock, shm, c->stream>>>(p, T, a, seed, t0, d_rew, d_flags, st, tiled, ot ? *ot : no_obs);
             };
             if (d_act) {
-                if (lds_table) launch(k_rollout<W, TB, false, true, EPW>, d_act);
-                else launch(k_rollout<W, TB, false, false, EPW>, d_act);
+                if (lds_table) launch(k_rollout<W, TB, false, true, EPW, OBS>, d_act);
+                else launch(k_rollout<W, TB, false, false, EPW, OBS>, d_act);
             } else {
-                if (lds_table) launch(k_rollout<W, TB, true, true, EPW>, nullptr);
-                else launch(k_rollout<W, TB, true, false, EPW>, nullptr);
+                if (lds_table) launch(k_rollout<W, TB, true, true, EPW, OBS>, nullptr);
+                else launch(k_rollout<W, TB, true, false, EPW, OBS>, nullptr);
             }
         };
-        if (half) go(std::integral_constant<int, 32>{});
-        else go(std::integral_constant<int, 64>{});
+        if (ot) go(std::integral_constant<int, 64>{}, std::true_type{});
+        else if (half) go(std::integral_constant<int, 32>{}, std::false_type{});
+        else go(std::integral_constant<int, 64>{}, std::false_type{});
+    });
+    return launch_check(c);
+}
+
+int check_obs_dims(Ctx* c, int32_t xd, int32_t yd) {
+    if (xd < 1 || yd < 1 || (uint32_t)xd * (uint32_t)yd > kObsCells)
+        return fail(c, SPARC_E_INVALID, "observation planes need x_dim, y_dim >= 1 and x_dim * y_dim <= 256");
+    return SPARC_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int sparc_rollout_device(void* ctx, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_t t0, int8_t* d_rew,
+                         uint8_t* d_flags, int32_t* d_stats) {
+    return rollout_impl(static_cast<Ctx*>(ctx), T, d_act, seed, t0, d_rew, d_flags, d_stats, nullptr);
+}
+
+int sparc_rollout_obs_device(void* ctx, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_t t0,
+                             int8_t* d_rew, uint8_t* d_flags, int32_t* d_stats, int32_t* d_visited,
+                             int32_t* d_agent, int32_t x_dim, int32_t y_dim) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c) return fail(nullptr, SPARC_E_INVALID, "null context");
+    int rc = check_obs_dims(c, x_dim, y_dim);
+    if (rc) return rc;
+    if (!d_visited && !d_agent) return rollout_impl(c, T, d_act, seed, t0, d_rew, d_flags, d_stats, nullptr);
+    const ObsTrace ot{d_visited, d_agent, (uint32_t)x_dim, (uint32_t)y_dim};
+    return rollout_impl(c, T, d_act, seed, t0, d_rew, d_flags, d_stats, &ot);
+}
+
+int sparc_step_obs_device(void* ctx, const uint8_t* d_act, int8_t* d_rew, uint8_t* d_flags, int32_t* d_visited,
+                          int32_t* d_agent, int32_t x_dim, int32_t y_dim, uint32_t* d_puzzle, uint32_t* d_xy) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    int rc = check_ctx(c, true);
+    if (rc) return rc;
+    if (!d_act || !d_rew || !d_flags) return fail(c, SPARC_E_INVALID, "null argument");
+    rc = check_obs_dims(c, x_dim, y_dim);
+    if (rc) return rc;
+    const Params p = make_params(c);
+    dispatch_w_tb(c->W, c->cfg.traceback, [&](auto w, auto tb) {
+        k_step_obs<decltype(w)::value, decltype(tb)::value><<<grid_for(c->n), kBlock, 0, c->stream>>>(
+            p, d_act, d_rew, d_flags, d_visited, d_agent, (uint32_t)x_dim, (uint32_t)y_dim, d_puzzle, d_xy);
     });
     return launch_check(c);
 }

@@ -144,6 +144,17 @@ class SparcCore:
         self._check(self.lib.sparc_rollout_device(self.ctx, int(T), d_actions, int(seed) & (2**64 - 1),
                                                   int(t0), d_reward, d_flags, d_stats))
 
+    def step_obs_device(self, d_actions, d_reward, d_flags, d_visited, d_agent, x_dim, y_dim, d_puzzle=None,
+                        d_xy=None):
+        self._check(self.lib.sparc_step_obs_device(self.ctx, d_actions, d_reward, d_flags, d_visited, d_agent,
+                                                   int(x_dim), int(y_dim), d_puzzle, d_xy))
+
+    def rollout_obs_device(self, T, d_actions, d_reward, d_flags, d_stats, d_visited, d_agent, x_dim, y_dim,
+                           seed=0, t0=0):
+        self._check(self.lib.sparc_rollout_obs_device(self.ctx, int(T), d_actions, int(seed) & (2**64 - 1),
+                                                      int(t0), d_reward, d_flags, d_stats, d_visited, d_agent,
+                                                      int(x_dim), int(y_dim)))
+
     def copy_state_device(self, which, d_out):
         self._check(self.lib.sparc_copy_state_device(self.ctx, int(which), d_out))
 

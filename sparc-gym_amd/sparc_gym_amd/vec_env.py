@@ -108,12 +108,17 @@ class SPaRCVecEnv:
         self.static_planes = torch.from_numpy(st).to(self.device)
 
     def _obs(self):
+        """Observation of the current state (after reset): separate copy / obs-pack launches."""
         self.core.copy_state_device(4, self._pidx.data_ptr())
         self.core.copy_state_device(1, self._pos.data_ptr())
+        if self.observation == "new":
+            self.core.obs_pack_device(self._vis.data_ptr(), self._agent.data_ptr(), self.x_dim, self.y_dim)
+        return self._obs_dict()
+
+    def _obs_dict(self):
         loc = torch.stack([self._pos & 0xFF, (self._pos >> 8) & 0xFF], dim=1)
         if self.observation == "compact":
             return {"puzzle_index": self._pidx, "agent_location": loc}
-        self.core.obs_pack_device(self._vis.data_ptr(), self._agent.data_ptr(), self.x_dim, self.y_dim)
         return {"visited": self._vis, "agent_location": self._agent, "puzzle_index": self._pidx,
                 "agent_xy": loc}
 
@@ -183,7 +188,12 @@ class SPaRCVecEnv:
             a = torch.where((a >= 0) & (a < 4), a, torch.full_like(a, 255)).to(torch.uint8)
         with torch.cuda.stream(s):
             self._act.copy_(a)
-        self.core.step_device(self._act.data_ptr(), self._rew.data_ptr(), self._flags.data_ptr())
+        # one launch: step + the post-step observation (k_step_obs)
+        new = self.observation == "new"
+        self.core.step_obs_device(self._act.data_ptr(), self._rew.data_ptr(), self._flags.data_ptr(),
+                                  self._vis.data_ptr() if new else None, self._agent.data_ptr() if new else None,
+                                  self.x_dim if new else 1, self.y_dim if new else 1,
+                                  self._pidx.data_ptr(), self._pos.data_ptr())
         f = self._flags
         reward = self._rew.to(torch.float64) / REWARD_SCALE
         terminated = (f & 1).bool()
@@ -191,13 +201,16 @@ class SPaRCVecEnv:
         info = {"legal_mask": (f >> 2) & 0xF, "autoreset": (f & 64).bool(), "reward_code": self._rew}
         if self.rules:
             info["rule_bits"] = self.rule_audit()["bits"]
-        return self._obs(), reward, terminated, truncated, info
+        return self._obs_dict(), reward, terminated, truncated, info
 
-    def rollout(self, T, actions=None, seed=0, t0=0, stats=None, record=True, out=None):
+    def rollout(self, T, actions=None, seed=0, t0=0, stats=None, record=True, out=None, obs=False, obs_out=None):
         """T steps of every env in ONE kernel launch.  actions: [T, N] uint8 on the GPU or None
         (counter-based random actions, sparc_rand_action(seed, env_offset + i, t0 + t)).
         Returns reward codes and flags [T, N] (int8 / uint8) if ``record`` (written into
-        ``out=(reward_code, flags)`` when given)."""
+        ``out=(reward_code, flags)`` when given).  With ``obs`` (or ``obs_out=(visited,
+        agent_location)``) the 'new' observation after every step is recorded too: int32
+        traces [T, N, x_dim, y_dim] under "visited" / "agent_location" (8 * x_dim * y_dim
+        bytes per env-step of HBM writes)."""
         self._stream()
         n = self.num_envs
         if actions is not None:
@@ -215,11 +228,24 @@ class SPaRCVecEnv:
             flags = torch.empty((T, n), dtype=torch.uint8, device=self.device)
         if stats is not None and (stats.shape != (n, 4) or stats.dtype != torch.int32 or not stats.is_contiguous()):
             raise ValueError("stats must be a contiguous int32 tensor [N, 4]")
-        self.core.rollout_device(T, None if actions is None else actions.data_ptr(),
-                                 None if rew is None else rew.data_ptr(),
-                                 None if flags is None else flags.data_ptr(),
-                                 None if stats is None else stats.data_ptr(), seed, t0)
-        return {"reward_code": rew, "flags": flags}
+        args = (None if actions is None else actions.data_ptr(), None if rew is None else rew.data_ptr(),
+                None if flags is None else flags.data_ptr(), None if stats is None else stats.data_ptr())
+        if not obs and obs_out is None:
+            self.core.rollout_device(T, *args, seed, t0)
+            return {"reward_code": rew, "flags": flags}
+        X, Y = self.x_dim, self.y_dim
+        if obs_out is not None:
+            vis, agent = obs_out
+            for t_ in (vis, agent):
+                if t_ is not None and (t_.shape != (T, n, X, Y) or t_.dtype != torch.int32 or
+                                       not t_.is_contiguous() or t_.device != self.device):
+                    raise ValueError(f"obs_out tensors must be contiguous int32 [{T}, {n}, {X}, {Y}] on {self.device}")
+        else:
+            vis = torch.empty((T, n, X, Y), dtype=torch.int32, device=self.device)
+            agent = torch.empty_like(vis)
+        self.core.rollout_obs_device(T, *args, None if vis is None else vis.data_ptr(),
+                                     None if agent is None else agent.data_ptr(), X, Y, seed, t0)
+        return {"reward_code": rew, "flags": flags, "visited": vis, "agent_location": agent}
 
     def state(self):
         """Host snapshot of the per-env state (x, y, path_len, step, puzzle, outcome, visited bits)."""

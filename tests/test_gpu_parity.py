@@ -347,3 +347,70 @@ def test_many_short_episodes_vs_oracle(on_gpu, max_steps):
     assert np.array_equal(r, ro) and np.array_equal(out["flags"].cpu().numpy(), fo)
     assert np.array_equal(st.cpu().numpy(), ost)
     assert (r == 100).sum() > 100        # the case needs solved episodes, and many of them
+
+
+# ----------------------------------------------------------------------------- 'new' obs traces
+@pytest.mark.parametrize("name", ["7x7_full", "mixed_5_11", "15x15"])
+@pytest.mark.parametrize("tb", [False, True])
+@pytest.mark.parametrize("n", [1001, 2048])
+def test_rollout_obs_and_step_obs_match_oracle(on_gpu, name, tb, n):
+    """rollout(obs=True) records the visited / agent_location planes after every step
+    (k_rollout OBS, cooperative 16-B stores); step() returns the same planes from k_step_obs.
+    Both bit-exact vs the oracle's planes, with autoresets inside the launch (max_steps 25)
+    and n = 1001 (partial last wave; n * x_dim * y_dim odd for 7x7 / 15x15, so odd steps take
+    the unaligned store path)."""
+    from sparc_gym_amd import SPaRCVecEnv
+    proc, table = _make(name, seed=11 + len(name))
+    T, ms = 48, 25
+    rng = np.random.default_rng(n + tb)
+    pids = rng.integers(len(proc), size=n)
+    acts = rng.choice(np.array([0, 1, 2, 3, 0, 1, 2, 3, 9], np.uint8), size=(T, n))
+    kw = dict(processed=proc, table=table, traceback=tb, max_steps=ms, observation="new")
+    a = SPaRCVecEnv(n, **kw)
+    a.reset(options={"puzzle_index": pids})
+    out = a.rollout(T, torch.from_numpy(acts).cuda(), obs=True)
+    X, Y = a.x_dim, a.y_dim
+    o = COracle(oracle_pool_from_processed(proc), n, tb, ms, autoreset=1)
+    o.reset(pids)
+    ro, fo, vo, ao = o.rollout_obs(T, X, Y, acts)
+    assert np.array_equal(out["reward_code"].cpu().numpy(), ro)
+    assert np.array_equal(out["flags"].cpu().numpy(), fo)
+    assert np.any(fo & 64)                                       # autoresets happened
+    assert np.array_equal(out["visited"].cpu().numpy(), vo)
+    assert np.array_equal(out["agent_location"].cpu().numpy(), ao)
+    b = SPaRCVecEnv(n, **kw)
+    b.reset(options={"puzzle_index": pids})
+    b_t = 0                                                      # steps b has taken
+    for t in range(0, T, 7 if n > 1500 else 1):
+        if t > b_t:
+            b.rollout(t - b_t, torch.from_numpy(acts[b_t:t]).cuda().contiguous())
+        obs, rew, term, trunc, info = b.step(torch.from_numpy(acts[t]).cuda())
+        b_t = t + 1
+        assert np.array_equal(info["reward_code"].cpu().numpy(), ro[t])
+        assert np.array_equal(obs["visited"].cpu().numpy(), vo[t]), t
+        assert np.array_equal(obs["agent_location"].cpu().numpy(), ao[t]), t
+        xy = obs["agent_xy"].cpu().numpy()
+        assert np.all(ao[t][np.arange(n), xy[:, 0], xy[:, 1]] == 1)
+
+
+def test_rollout_obs_only_one_plane_and_chunks(on_gpu):
+    """Either trace may be omitted; chunked obs rollouts equal one launch."""
+    from sparc_gym_amd import SPaRCVecEnv
+    proc, table = _make("mixed_5_11", seed=4)
+    n, T = 4096, 40
+    acts = torch.randint(0, 4, (T, n), dtype=torch.uint8, device="cuda")
+    kw = dict(processed=proc, table=table, traceback=True, observation="new")
+    a = SPaRCVecEnv(n, **kw)
+    a.reset(seed=1)
+    full = a.rollout(T, acts, obs=True)
+    b = SPaRCVecEnv(n, **kw)
+    b.reset(seed=1)
+    X, Y = b.x_dim, b.y_dim
+    vis1 = torch.full((16, n, X, Y), -7, dtype=torch.int32, device="cuda")
+    p1 = b.rollout(16, acts[:16].contiguous(), obs_out=(vis1, None))
+    p2 = b.rollout(T - 16, acts[16:].contiguous(), obs=True)
+    assert p1["agent_location"] is None
+    assert torch.equal(full["visited"][:16], vis1)
+    assert torch.equal(full["visited"][16:], p2["visited"])
+    assert torch.equal(full["agent_location"][16:], p2["agent_location"])
+    assert torch.equal(full["flags"], torch.cat([p1["flags"], p2["flags"]]))

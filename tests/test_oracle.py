@@ -67,3 +67,25 @@ def test_rand_action_distribution():
     a = np.array([o.rand_action(7, e, t) for e in range(64) for t in range(64)])
     assert set(np.unique(a)) == {0, 1, 2, 3}
     assert abs(np.bincount(a).min() - len(a) / 4) < 0.1 * len(a)
+
+
+@pytest.mark.parametrize("pool", golden_io.POOLS)
+def test_c_oracle_obs_planes_match_reference(pool):
+    """oracle_rollout_obs's per-step visited / agent_location planes == the reference's
+    obs['base'] planes after every step (SPaRC_Gym.py:956-979), padded to 16x16."""
+    g = golden_io.load(pool)
+    puzzles = golden_io.oracle_puzzles(g)
+    eps = g["episodes"]
+    T = max(len(e["actions"]) for e in eps)
+    o = COracle(puzzles, len(eps), g["traceback"], g["max_steps"], autoreset=0)
+    o.reset([e["puzzle_index"] for e in eps])
+    acts = np.zeros((T, len(eps)), np.uint8)
+    for i, e in enumerate(eps):
+        acts[:len(e["actions"]), i] = e["actions"]
+    _, _, vis, agent = o.rollout_obs(T, 16, 16, acts)
+    for i, e in enumerate(eps):
+        for t, st in enumerate(e["steps"]):
+            X, Y = st["visited"]["shape"]
+            assert np.array_equal(vis[t, i, :X, :Y], golden_io.dense(st["visited"])), (pool, i, t)
+            assert np.array_equal(agent[t, i, :X, :Y], golden_io.dense(st["agent_plane"])), (pool, i, t)
+            assert vis[t, i].sum() == vis[t, i, :X, :Y].sum() and agent[t, i].sum() == 1

@@ -29,7 +29,7 @@ ap.add_argument("--no-out", action="store_true", help="do not write reward codes
 ap.add_argument("--time", action="store_true", help="print the mean launch time (HIP events)")
 ap.add_argument("--lib", default=None, help="path of a diagnostic build of libsparc_gym_amd.so")
 a = ap.parse_args()
-sizes, full, tb = bench.CONFIGS[a.config]
+sizes, full, tb, obs = bench.CONFIGS[a.config]
 proc = process_puzzles(synthetic.make_puzzles(1024, seed=0, sizes=sizes, full_properties=full))
 table = pack_table(proc)
 vec = SPaRCVecEnv(a.envs, processed=proc, table=table, traceback=tb, observation="compact")
@@ -39,6 +39,10 @@ acts = torch.randint(0, 4, (a.launches + 1, a.chunk, a.envs), dtype=torch.uint8,
 rew = torch.empty((a.chunk, a.envs), dtype=torch.int8, device="cuda")
 flg = torch.empty((a.chunk, a.envs), dtype=torch.uint8, device="cuda")
 stats = torch.zeros((a.envs, 4), dtype=torch.int32, device="cuda")
+ovis = oag = None
+if obs:   # c4: 'new' observation traces [chunk, N, x_dim, y_dim] int32, as bench.py
+    ovis = torch.empty((a.chunk, a.envs, vec.x_dim, vec.y_dim), dtype=torch.int32, device="cuda")
+    oag = torch.empty_like(ovis)
 ms = []
 for k in range(a.launches + 1):      # first launch = warmup
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -46,7 +50,8 @@ for k in range(a.launches + 1):      # first launch = warmup
     if a.no_out:
         vec.rollout(a.chunk, None if a.rand else acts[k], stats=stats, record=False, seed=k)
     else:
-        vec.rollout(a.chunk, None if a.rand else acts[k], stats=stats, out=(rew, flg), seed=k)
+        vec.rollout(a.chunk, None if a.rand else acts[k], stats=stats, out=(rew, flg), seed=k,
+                    obs_out=(ovis, oag) if obs else None)
     e1.record()
     ms.append((e0, e1))
 torch.cuda.synchronize()

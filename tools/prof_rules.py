@@ -27,7 +27,7 @@ ap.add_argument("--launches", type=int, default=10)
 ap.add_argument("--rule-pool", action="store_true", help="rule-consistent puzzles instead of the bench pool")
 ap.add_argument("--lib", default=None, help="path of a diagnostic build of libsparc_gym_amd.so")
 a = ap.parse_args()
-sizes, full, tb = bench.CONFIGS[a.config]
+sizes, full, tb, obs = bench.CONFIGS[a.config]
 recs = (synthetic.make_rule_puzzles(1024, seed=0, sizes=sizes) if a.rule_pool
         else synthetic.make_puzzles(1024, seed=0, sizes=sizes, full_properties=full))
 proc = process_puzzles(recs)
