@@ -234,7 +234,13 @@ def main():
     per_step = 3 + (2 * plane_bytes if obs and args.mode == "rollout" else 0)
     bytes_launch = n * (per_step * avg_T + per_env_launch)
     achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
-    kernel = ("k_rollout1" if table.words == 1 and not obs else "k_rollout") if args.mode == "rollout" else "k_step"
+    if args.mode != "rollout":
+        kernel = "k_step"
+    elif table.words == 1 and not obs:
+        # traceback batches of whole 256-env workgroups: the split move / trie kernel
+        kernel = "k_rollout1s" if tb and n % 256 == 0 and chunk >= 16 else "k_rollout1"
+    else:
+        kernel = "k_rollout"
     workload = f"{args.config}_{args.mode}_n{n}_chunk{chunk if args.mode == 'rollout' else 1}"
     traffic = load_traffic(workload, kernel)
     out = {

@@ -592,6 +592,11 @@ struct Env<1, TB, Stack> {
         return f;
     }
 
+    // COND_GATHER: gather the record only for lanes whose node moved (exec-masked; most waves
+    // skip it).  The branch costs ~5% with one wave per SIMD, where the unconditional gather's
+    // latency is hidden anyway; with two waves per SIMD the gathers themselves are the limit
+    // (MI355X, c3: 2.24e11 -> 2.94e11 env-steps/s at 131,072 envs), so the split kernel uses it.
+    template <bool COND_GATHER = false>
     __device__ __forceinline__ int phase_trie(const Params& p) {
         // a reset step starts the new puzzle's trie at its root
         nn = pick(s_rs != 0u, ((pflags >> 3) & 1u) << 15, nn);
@@ -607,7 +612,8 @@ struct Env<1, TB, Stack> {
         nn = pick(down, c, pick(up, rec.z, nn));
         off = pick(on, s_fwd & (uint32_t)!has, off + s_fwd - s_pop);
 #ifndef SPARC_DIAG_NO_TRIE_LOAD
-        load_rec(p);
+        // the record changes only with the node (a random walk is off the trie on most steps)
+        if (!COND_GATHER || (down | up | (s_rs != 0u))) load_rec(p);
 #endif
         // reward code (1204-1223): done: +100 on a solution, else -100 unless the previous
         // done step already set outcome_reward = 1 (then 0); otherwise +-1 when moved (0 if the
@@ -628,6 +634,40 @@ struct Env<1, TB, Stack> {
         flags = phase_move(p, a);
         was_reset = s_rs;
         return phase_trie(p);
+    }
+
+    // ---- k_rollout1s: the step split over a move wave (reset_next + phase_move) and a trie
+    // wave (phase_trie).  The move wave hands each step's trie inputs over as one byte:
+    // action | forward << 2 | pop << 3 | moved-with-solutions << 4 | done << 5 | reset << 6
+    __device__ __forceinline__ uint32_t hand_byte() const {
+        return (s_a & 3u) | (s_fwd << 2) | (s_pop << 3) | (s_mv << 4) | (s_done << 5) | (s_rs << 6);
+    }
+    // the trie wave's side: unpack the byte; a reset step moves to the next puzzle's rows, as
+    // the move wave's reset_next did for its part (index + 1 mod P, SPaRC_Gym.py:1087)
+    template <class Src>
+    __device__ __forceinline__ void take_hand(const Src& src, uint32_t num_puzzles, uint32_t hb) {
+        s_a = hb & 3u;
+        s_fwd = (hb >> 2) & 1u;
+        s_pop = (hb >> 3) & 1u;
+        s_mv = (hb >> 4) & 1u;
+        s_done = (hb >> 5) & 1u;
+        s_rs = hb >> 6;
+        if (s_rs) {
+            pid = pid + 1 == num_puzzles ? 0u : pid + 1;
+            (void)load_puzzle(src, pid);
+        }
+    }
+    // the trie wave's part of load(): puzzle rows, trie state and the node's record
+    template <class Src>
+    __device__ __forceinline__ void load_trie(const Params& p, const Src& src, uint32_t i) {
+        const State& s = p.st;
+        const uint32_t ps = s.pos[i], ax = s.aux[i];
+        off = ps >> 24;
+        nn = (ax & 0x7FFFu) | (((ax >> 19) & 1u) << 15);
+        outcome = (ax >> 16) & 3u;
+        pid = s.pid[i];
+        (void)load_puzzle(src, pid);
+        load_rec(p);
     }
 
     // the code and solved flag that phase_trie would report again for the last step of the

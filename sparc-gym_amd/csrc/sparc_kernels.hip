@@ -248,6 +248,7 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
                                                     uint8_t* __restrict__ flg, int4* __restrict__ stats,
                                                     uint32_t tiled, ObsTrace ot) {
     static_assert(!OBS || EPW == 64, "the observation writer needs full 64-lane waves");
+    constexpr int kUnrollSteps = OBS ? 1 : 4;   // OBS: one step body (its plane writer is long)
     // LDS: [I/O tiles, 3*16*EPW B per wave][W=1 traceback: move stacks, 64*EPW B per wave][rows]
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -339,7 +340,7 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
                     av[j] = RAND ? uint_rand_action(seed, gid, t0 + (uint64_t)(tb + g + j)) : ta[(g + j) * EPW + lane];
-#pragma unroll(OBS ? 1 : 4)
+#pragma unroll kUnrollSteps
                 for (int j = 0; j < 4; ++j) {
                     const int k = g + j;
                     uint32_t f;
@@ -585,6 +586,180 @@ __global__ void __launch_bounds__(kBlock1) k_rollout1(Params p, int32_t T, const
         st.z += acc.z;
         st.w += acc.w;
         stats[i] = st;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// W = 1 rollout with each env's step split over TWO waves (k_rollout1s).
+//
+// A lone wave issues one instruction every ~5 cycles while its SIMD can take one every ~2.5
+// from two waves, and at 65,536 envs there is exactly one 64-env wave per SIMD.  So the step is
+// cut where its data flow is one-way: a MOVE wave runs the autoreset, legality, move, path and
+// flags (reset_next + phase_move) and hands each env-step's trie inputs to a TRIE wave as one
+// LDS byte (hand_byte); the trie wave runs the solution-trie transition, the record gather and
+// the reward code (phase_trie) one 16-step tile behind.  Nothing flows back: the reward code
+// never feeds the move.  The I/O wave streams action tiles in and reward / flag tiles out as in
+// k_rollout1.  Per workgroup 256 envs = 4 move waves (0-3) + 4 trie waves (4-7, on the same
+// SIMDs as the move waves of their envs) + 1 I/O wave; one barrier per tile:
+//   interval k (between barriers B_k and B_k+1): move waves step tile k; trie waves finish
+//   tile k-1; the I/O wave loads the actions of tile k+1 and stores the outputs of tile k-2.
+// Only full workgroups, T % 16 == 0 and 16-B aligned I/O; the host runs any tail through
+// k_rollout1.  The state after the launch is the same SoA record (the trie wave hands its
+// final node / depth / outcome and stats to the move wave through LDS before the store).
+constexpr int kBlock1s = 576;
+constexpr size_t kS_Act = 0;                          // actions [2 tiles][16][64]
+constexpr size_t kS_Rew = kS_Act + 2 * kTile * 64;    // reward ring [64 steps][64]
+constexpr size_t kS_Flg = kS_Rew + kRing * 64;        // flag ring [64][64]
+constexpr size_t kS_Hand = kS_Flg + kRing * 64;       // hand-over ring [64][64] (flag ring rows)
+constexpr size_t kS_Stk = kS_Hand + kRing * 64;       // move stack [64 moves][64]
+constexpr size_t kS_Pair = kS_Stk + 64 * 64;          // per move / trie wave pair
+constexpr size_t kS_Fin = 4 * kS_Pair;                // trie wave's final state [4][64] uint4
+constexpr size_t kS_Base = kS_Fin + 4 * 64 * sizeof(uint4);
+
+template <bool TB, bool RAND, bool LDS_TABLE>
+__global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, const uint8_t* __restrict__ act,
+                                                        uint64_t seed, uint64_t t0, int8_t* __restrict__ rew,
+                                                        uint8_t* __restrict__ flg, int4* __restrict__ stats) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    PuzzleSrc<1> src{p.tab.info, p.tab.root, p.tab.open, p.tab.init, p.tab.row1};
+    if constexpr (LDS_TABLE) {
+        const uint32_t P = p.tab.num_puzzles;
+        uint4* lrow1 = reinterpret_cast<uint4*>(smem + kS_Base);
+        uint64_t* linit = reinterpret_cast<uint64_t*>(lrow1 + P);
+        for (uint32_t k = threadIdx.x; k < P; k += kBlock1s) {
+            lrow1[k] = p.tab.row1[k];
+            linit[k] = p.tab.init[k];
+        }
+        __syncthreads();
+        src = PuzzleSrc<1>{p.tab.info, p.tab.root, p.tab.open, linit, lrow1};
+    }
+    const size_t n = p.n;
+    const uint32_t wg_base = blockIdx.x * 256u;
+    const int32_t K = T / kTile;
+
+    if (wv == 8) {                                               // ---- the I/O wave
+        const uint32_t r = lane >> 2, c = (lane & 3u) * 16u;
+        auto load_tile = [&](int32_t k) {                        // actions of tile k -> buffer k & 1
+            if constexpr (!RAND) {
+                u32x4 v[4];
+#pragma unroll
+                for (int w = 0; w < 4; ++w) v[w] = nt_load16(act + (size_t)(k * kTile + r) * n + wg_base + w * 64 + c);
+#pragma unroll
+                for (int w = 0; w < 4; ++w)
+                    *reinterpret_cast<u32x4*>(smem + w * kS_Pair + kS_Act + (k & 1) * (kTile * 64) + r * 64 + c) = v[w];
+            }
+        };
+        auto store_tile = [&](int32_t k) {                       // whole 128-B lines, as k_rollout1
+            const uint32_t r8 = lane >> 3, c8 = (lane & 7u) * 16u;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const uint32_t row = (uint32_t)((k * kTile) & (kRing - 1)) + h * 8 + r8;
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const int w = 2 * q + (int)(c8 >> 6);
+                    const uint8_t* base = smem + w * kS_Pair + row * 64 + (c8 & 63u);
+                    const size_t o = (size_t)(k * kTile + h * 8 + r8) * n + wg_base + q * 128 + c8;
+                    if (rew) nt_store16(reinterpret_cast<uint8_t*>(rew) + o, *reinterpret_cast<const u32x4*>(base + kS_Rew));
+                    if (flg) nt_store16(flg + o, *reinterpret_cast<const u32x4*>(base + kS_Flg));
+                }
+            }
+        };
+        if (K > 0) load_tile(0);
+        __syncthreads();                                         // B_0
+        for (int32_t k = 0; k <= K; ++k) {
+            if (k + 1 < K) load_tile(k + 1);
+            if (k >= 2) store_tile(k - 2);
+            __syncthreads();                                     // B_{k+1}
+        }
+        if (K >= 1) store_tile(K - 1);
+        __syncthreads();                                         // B_{K+2}
+        return;
+    }
+
+    const uint32_t pr = wv & 3u;                                 // the pair's 64 envs
+    const uint32_t i = wg_base + pr * 64u + lane;
+    uint8_t* pb = smem + pr * kS_Pair;
+    uint4* fin = reinterpret_cast<uint4*>(smem + kS_Fin) + pr * 64u + lane;
+    using Stack = typename std::conditional<TB, LdsStack<64>, RegStack>::type;
+    Env<1, TB, Stack> e;
+    if (wv < 4) {                                                // ---- move waves
+        if constexpr (TB) e.stk.col = pb + kS_Stk + lane;
+        e.load(p, src, i);
+        const uint64_t gid = p.env_offset + i;
+        uint8_t* tf = pb + kS_Flg + lane;
+        int acc_y = 0, acc_w = 0;
+        __syncthreads();                                         // B_0
+        for (int32_t k = 0; k < K; ++k) {
+            const uint8_t* ta = pb + kS_Act + (k & 1) * (kTile * 64) + lane;
+#ifdef SPARC_DIAG_SPLIT_MOVE_IDLE
+            if (k >= 0) {
+                __syncthreads();
+                continue;
+            }
+#endif
+#pragma unroll 1
+            for (int g = 0; g < kTile; g += 4) {
+                uint32_t av[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    av[j] = RAND ? uint_rand_action(seed, gid, t0 + (uint64_t)(k * kTile + g + j)) : ta[(g + j) * 64];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t row = (uint32_t)(k * kTile + g + j) & (kRing - 1);
+                    e.reset_next(p, src);
+                    const uint32_t f = e.phase_move(p, av[j]);
+                    tf[row * 64] = (uint8_t)f;
+                    tf[row * 64 + (kS_Hand - kS_Flg)] = (uint8_t)e.hand_byte();
+                    acc_y += (int)e.pending;
+                    acc_w += (int)e.s_rs;
+                }
+            }
+            __syncthreads();                                     // B_{k+1}
+        }
+        __syncthreads();                                         // B_{K+1}
+        __syncthreads();                                         // B_{K+2}: the trie state is in fin
+        const uint4 fs = *fin;
+        e.nn = fs.x & 0xFFFFu;
+        e.outcome = fs.x >> 16;
+        e.off = fs.y;
+        e.store(p, src, i);
+        if (stats) {
+            int4 st = stats[i];
+            st.x += (int)fs.z;
+            st.y += acc_y;
+            st.z += (int)fs.w;
+            st.w += acc_w;
+            stats[i] = st;
+        }
+    } else {                                                     // ---- trie waves
+        e.load_trie(p, src, i);
+        const uint8_t* th = pb + kS_Hand + lane;
+        uint8_t* tr = pb + kS_Rew + lane;
+        int acc_x = 0;
+        uint32_t acc_z = 0;
+        __syncthreads();                                         // B_0
+        __syncthreads();                                         // B_1 (interval 0: no tile yet)
+        for (int32_t k = 1; k <= K; ++k) {
+#ifdef SPARC_DIAG_SPLIT_TRIE_IDLE
+            if (k >= 0) {
+                __syncthreads();
+                continue;
+            }
+#endif
+#pragma unroll 4
+            for (int s = 0; s < kTile; ++s) {
+                const uint32_t row = (uint32_t)((k - 1) * kTile + s) & (kRing - 1);
+                e.take_hand(src, p.tab.num_puzzles, th[row * 64]);
+                const int code = e.template phase_trie<true>(p);
+                tr[row * 64] = (uint8_t)code;
+                acc_x += code;
+                acc_z += e.solved;
+            }
+            __syncthreads();                                     // B_{k+1}
+        }
+        *fin = make_uint4(e.nn | (e.outcome << 16), e.off, (uint32_t)acc_x, acc_z);
+        __syncthreads();                                         // B_{K+2}
     }
 }
 
@@ -1048,6 +1223,42 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
         const size_t per_cu = (blocks + 255) / 256;
         const size_t budget = std::min(kMaxDynLds, (size_t)160 * 1024 / (per_cu ? per_cu : 1));
         const size_t tbytes = table_lds_bytes<1>(c->num_puzzles);
+#ifndef SPARC_EXP_NO_SPLIT
+        // traceback: the full tiles of full workgroups go through the split move / trie kernel
+        // (MI355X, c3 at 65,536 envs: 0.295 vs 0.312 ms per 1,000 steps); a tail of T % 16 steps
+        // or a batch that is not a multiple of 256 envs goes through k_rollout1 below.  Without
+        // traceback the move wave is lighter and the fused kernel is as fast (c2: 0.289 vs 0.297).
+        if (c->cfg.traceback && tiled && c->n % 256 == 0 && T >= kTile) {
+            const int32_t T16 = T / kTile * kTile;
+            const bool lds_s = kS_Base + tbytes <= budget;
+            const size_t shm_s = kS_Base + (lds_s ? tbytes : 0);
+            auto launch_s = [&](auto kern, const uint8_t* a) {
+                if (shm_s > 64 * 1024)
+                    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm_s);
+                kern<<<dim3((unsigned)blocks), kBlock1s, shm_s, c->stream>>>(p, T16, a, seed, t0, d_rew, d_flags, st);
+            };
+            auto go_s = [&](auto tb) {
+                constexpr bool TB = decltype(tb)::value;
+                if (d_act) {
+                    if (lds_s) launch_s(k_rollout1s<TB, false, true>, d_act);
+                    else launch_s(k_rollout1s<TB, false, false>, d_act);
+                } else {
+                    if (lds_s) launch_s(k_rollout1s<TB, true, true>, nullptr);
+                    else launch_s(k_rollout1s<TB, true, false>, nullptr);
+                }
+            };
+            go_s(std::true_type{});
+            rc = launch_check(c);
+            if (rc || T16 == T) return rc;
+            const size_t adv = (size_t)T16 * c->n;
+            if (d_act) d_act += adv;
+            if (d_rew) d_rew += adv;
+            if (d_flags) d_flags += adv;
+            t0 += (uint64_t)T16;
+            T -= T16;
+        }
+#endif
         const bool lds_table = kW1Base + tbytes <= budget;
         const size_t shm = kW1Base + (lds_table ? tbytes : 0);
         auto launch = [&](auto kern, const uint8_t* a) {

@@ -264,12 +264,14 @@ def test_device_reset_rejects_bad_index(on_gpu):
         v.core.sync()
 
 
-@pytest.mark.parametrize("n", [2624, 3000])
+@pytest.mark.parametrize("n", [2560, 2624, 3000])
 def test_w1_chunked_partial_workgroups(on_gpu, n):
-    """k_rollout1 (W = 1): full workgroups through the I/O wave next to a partial last workgroup
-    (n = 2624: n % 16 == 0, tiled) or every workgroup on the direct path (n = 3000: untiled);
-    launches of 100 + 57 + 1 + 32 steps (tails, single steps, exact tiles) equal one launch of
-    190 steps, reward codes, flags and per-env stats alike, and equal the oracle."""
+    """W = 1 rollouts: n = 2560 (a multiple of 256) runs the full tiles through the split move /
+    trie kernel k_rollout1s and the T % 16 tail through k_rollout1; n = 2624 (n % 16 == 0,
+    tiled) runs k_rollout1's full workgroups through the I/O wave next to a partial last
+    workgroup; n = 3000 runs every workgroup on the direct path (untiled).  Launches of
+    100 + 57 + 1 + 32 steps (tails, single steps, exact tiles) equal one launch of 190 steps,
+    reward codes, flags and per-env stats alike, and equal the oracle."""
     from sparc_gym_amd import SPaRCVecEnv
     proc, table = _make("7x7_full", seed=9)
     assert table.words == 1
