@@ -20,6 +20,7 @@ import argparse
 import json
 import os
 import platform
+import subprocess
 import sys
 import time
 
@@ -66,7 +67,7 @@ def state_bytes_per_env(words, traceback):
     return 8 * words + (16 * words if traceback else 0) + 16
 
 
-def cpu_baseline(proc, tb, max_steps, seconds, obs_dims=None):
+def cpu_baseline(proc, tb, max_steps, seconds, obs_dims=None, config="c3"):
     """C oracle (sparc_oracle.c, 1 thread) on a bounded sample of the same workload (with
     obs_dims = (x_dim, y_dim): also writing the 'new' observation planes of every step)."""
     from oracle import COracle
@@ -98,14 +99,29 @@ def cpu_baseline(proc, tb, max_steps, seconds, obs_dims=None):
             env.p = pool[k % len(pool)]
             env.reset()
     py_rate = k / (time.perf_counter() - t1)
-    return {"value": round(c_rate, 1), "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/sparc_oracle.c, {n} envs x {steps} steps, random actions, next-step autoreset, "
-                      f"{'visited + agent_location planes written every step, ' if obs_dims else ''}"
-                      f"1 thread, {dt:.1f} s; CPU {platform.processor() or platform.machine()}, "
-                      f"os.cpu_count()={os.cpu_count()}",
-            "python_port_value": round(py_rate, 1),
-            "python_port_sample": "oracle/cpu_ref.py (reference step() restated in pure Python, no rule "
-                                  f"audit), 1 env, {k} steps, 1 thread"}
+    out = {"value": round(c_rate, 1), "unit": "env-steps/s", "cores": 1, "kind": "port",
+           "sample": f"oracle/sparc_oracle.c, {n} envs x {steps} steps, random actions, next-step autoreset, "
+                     f"{'visited + agent_location planes written every step, ' if obs_dims else ''}"
+                     f"1 thread, {dt:.1f} s; CPU {platform.processor() or platform.machine()}, "
+                     f"os.cpu_count()={os.cpu_count()}",
+           "value_1core": round(c_rate, 1),
+           "python_port_value": round(py_rate, 1),
+           "python_port_sample": "oracle/cpu_ref.py (reference step() restated in pure Python, no rule "
+                                 f"audit), 1 env, {k} steps, 1 thread"}
+    # the same oracle, one process per core (BASELINE.md CPU-baseline plan), in a child process
+    # that never touches the GPU; up to 16 cores (one GPU's share of the box)
+    cmd = [sys.executable, "-m", "oracle.cpu_bench", "--config", config, "--seconds", str(seconds),
+           "--max-steps", str(max_steps)] + (["--obs", str(obs_dims[0]), str(obs_dims[1])] if obs_dims else [])
+    try:
+        r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=seconds * 4 + 120)
+        mc = json.loads(r.stdout.strip().splitlines()[-1])
+        out.update(value=mc["value"], cores=mc["procs"],
+                   sample=out["sample"] +
+                   f"; all-cores value: {mc['procs']} processes x {n} envs (oracle/cpu_bench.py), "
+                   f"{mc['seconds']:.0f} s, {mc['usable_cores']} usable cores")
+    except (subprocess.SubprocessError, ValueError, KeyError, IndexError) as exc:   # keep the 1-core number
+        out["multi_core_error"] = repr(exc)[:200]
+    return out
 
 
 def load_traffic(workload, kernel):
@@ -276,7 +292,7 @@ def main():
         "episodes": summary,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb = cpu_baseline(proc, tb, args.max_steps, args.cpu_seconds, (X, Y) if obs else None)
+        cb = cpu_baseline(proc, tb, args.max_steps, args.cpu_seconds, (X, Y) if obs else None, args.config)
         out["cpu_baseline"] = cb
         out["gpu_vs_cpu"] = round(value / cb["value"], 1)
     elif rank == 0:
