@@ -253,8 +253,8 @@ def main():
     if args.mode != "rollout":
         kernel = "k_step"
     elif table.words == 1 and not obs:
-        # traceback batches of whole 256-env workgroups: the split move / trie kernel
-        kernel = "k_rollout1s" if tb and n % 256 == 0 and chunk >= 16 else "k_rollout1"
+        # batches of whole 256-env workgroups: the split move / trie kernel
+        kernel = "k_rollout1s" if n % 256 == 0 and chunk >= 16 else "k_rollout1"
     else:
         kernel = "k_rollout"
     workload = f"{args.config}_{args.mode}_n{n}_chunk{chunk if args.mode == 'rollout' else 1}"

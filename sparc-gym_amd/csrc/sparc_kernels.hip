@@ -733,6 +733,12 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
             stats[i] = st;
         }
     } else {                                                     // ---- trie waves
+#ifndef SPARC_EXP_TRIE_NOPRIO
+        // the trie wave wins VALU arbitration against its (older) move wave partner: its chain
+        // carries the record-gather waits, the move wave has slack (c3: 0.289 -> 0.266 ms per
+        // 1,000 steps; priority to the move wave instead: no change)
+        __builtin_amdgcn_s_setprio(1);
+#endif
         e.load_trie(p, src, i);
         const uint8_t* th = pb + kS_Hand + lane;
         uint8_t* tr = pb + kS_Rew + lane;
@@ -747,14 +753,21 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
                 continue;
             }
 #endif
-#pragma unroll 4
-            for (int s = 0; s < kTile; ++s) {
-                const uint32_t row = (uint32_t)((k - 1) * kTile + s) & (kRing - 1);
-                e.take_hand(src, p.tab.num_puzzles, th[row * 64]);
-                const int code = e.template phase_trie<true>(p);
-                tr[row * 64] = (uint8_t)code;
-                acc_x += code;
-                acc_z += e.solved;
+#pragma unroll 1
+            for (int g = 0; g < kTile; g += 4) {
+                // the group's 4 hand-over bytes first (one LDS wait), then its 4 steps
+                const uint32_t row0 = (uint32_t)((k - 1) * kTile + g) & (kRing - 1);
+                uint32_t hb[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) hb[j] = th[(row0 + j) * 64];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    e.take_hand(src, p.tab.num_puzzles, hb[j]);
+                    const int code = e.template phase_trie<true>(p);
+                    tr[(row0 + j) * 64] = (uint8_t)code;
+                    acc_x += code;
+                    acc_z += e.solved;
+                }
             }
             __syncthreads();                                     // B_{k+1}
         }
@@ -1224,11 +1237,10 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
         const size_t budget = std::min(kMaxDynLds, (size_t)160 * 1024 / (per_cu ? per_cu : 1));
         const size_t tbytes = table_lds_bytes<1>(c->num_puzzles);
 #ifndef SPARC_EXP_NO_SPLIT
-        // traceback: the full tiles of full workgroups go through the split move / trie kernel
-        // (MI355X, c3 at 65,536 envs: 0.295 vs 0.312 ms per 1,000 steps); a tail of T % 16 steps
-        // or a batch that is not a multiple of 256 envs goes through k_rollout1 below.  Without
-        // traceback the move wave is lighter and the fused kernel is as fast (c2: 0.289 vs 0.297).
-        if (c->cfg.traceback && tiled && c->n % 256 == 0 && T >= kTile) {
+        // the full tiles of full workgroups go through the split move / trie kernel (MI355X, c3
+        // at 65,536 envs: 0.266 vs 0.312 ms per 1,000 steps); a tail of T % 16 steps or a batch
+        // that is not a multiple of 256 envs goes through k_rollout1 below
+        if (tiled && c->n % 256 == 0 && T >= kTile) {
             const int32_t T16 = T / kTile * kTile;
             const bool lds_s = kS_Base + tbytes <= budget;
             const size_t shm_s = kS_Base + (lds_s ? tbytes : 0);
@@ -1248,7 +1260,8 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
                     else launch_s(k_rollout1s<TB, true, false>, nullptr);
                 }
             };
-            go_s(std::true_type{});
+            if (c->cfg.traceback) go_s(std::true_type{});
+            else go_s(std::false_type{});
             rc = launch_check(c);
             if (rc || T16 == T) return rc;
             const size_t adv = (size_t)T16 * c->n;
