@@ -416,3 +416,26 @@ def test_rollout_obs_only_one_plane_and_chunks(on_gpu):
     assert torch.equal(full["visited"][16:], p2["visited"])
     assert torch.equal(full["agent_location"][16:], p2["agent_location"])
     assert torch.equal(full["flags"], torch.cat([p1["flags"], p2["flags"]]))
+
+
+def test_obs_entry_points_validate_plane_dims(on_gpu):
+    """x_dim * y_dim > 256 (the plane writer's cell LUT) and x_dim < 1 are rejected with
+    ValueError before any launch; a valid call still works afterwards."""
+    from sparc_gym_amd import SPaRCVecEnv
+    proc, table = _make("7x7_full", seed=12)
+    n = 128
+    v = SPaRCVecEnv(n, processed=proc, table=table, observation="compact")
+    v.reset(seed=0)
+    a = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    r = torch.empty(n, dtype=torch.int8, device="cuda")
+    f = torch.empty(n, dtype=torch.uint8, device="cuda")
+    planes = torch.empty(n * 17 * 17, dtype=torch.int32, device="cuda")
+    for xd, yd in ((17, 17), (0, 7)):
+        with pytest.raises(ValueError):
+            v.core.step_obs_device(a.data_ptr(), r.data_ptr(), f.data_ptr(), planes.data_ptr(), None, xd, yd)
+        with pytest.raises(ValueError):
+            v.core.rollout_obs_device(1, a.data_ptr(), r.data_ptr(), f.data_ptr(), None, planes.data_ptr(), None, xd, yd)
+    v.core.step_obs_device(a.data_ptr(), r.data_ptr(), f.data_ptr(), planes.data_ptr(), None, 7, 7)
+    torch.cuda.synchronize()
+    vis = planes[:n * 49].view(n, 7, 7).cpu().numpy()
+    assert vis.reshape(n, -1).sum(1).min() >= 1          # the start (and any move) is visited
