@@ -4,14 +4,21 @@
 Workload (default, BASELINE.json configs[2]): 65,536 concurrent 7x7 SPaRC instances per GPU,
 full property set, traceback=True, max_steps=2000, gymnasium next-step autoreset onto the next
 puzzle, 1,024 synthetic puzzles (seed 0), env i -> puzzle (i * 2654435761) mod 1024.
-One bench "step" = every env advanced by one env.step().  Actions are uniform random in
-{0,1,2,3}, generated on the GPU before the timed region ([K, N] uint8 resident in HBM, like a
-policy's output).  The timed region runs K steps as ceil(K / chunk) launches of the fused
-rollout kernel (state in VGPRs, per-step reward codes + flags streamed to HBM), then the
-end-of-batch gather of per-env (reward sum, dones, solved, resets) to rank 0 over RCCL.
-``--mode step`` instead times one k_step launch per env-step (the gym one-call-per-step contract).
+Actions are uniform random in {0,1,2,3}, generated on the GPU before the timed region (uint8
+tiles resident in HBM, like a policy's output).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs 65536] [--chunk 500]
+One bench "step" is one pass of the hot path over the batch: one rollout launch that advances
+every env by ``--env-steps`` T env.step()s (default 2,000; 50 for c4, whose launch also writes
+the 'new' planes of every step), state in VGPRs, per-step reward codes + flags streamed to HBM.
+The timed region runs K such launches back to back, then the end-of-batch gather of per-env
+(reward sum, dones, solved, resets) to every rank over RCCL.  ``value`` = all env-steps of all
+ranks / the slowest rank's time.  ``--mode step`` instead times one k_step launch per bench
+step (T = 1, the gym one-call-per-step contract).
+
+Buffers: K launches cycle through up to 8 distinct action tiles [T, N] and 2 output tiles (a
+consumer reads each launch's outputs before the next one but one), so any K fits in HBM.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs 65536] [--env-steps 2000]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU)
 """
 from __future__ import annotations
@@ -44,13 +51,13 @@ DEFAULT_ENVS = {"c2": 4096, "c3": 65536, "c4": 262144}
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2000)
-    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=20, help="timed bench steps (rollout launches of T env-steps)")
+    ap.add_argument("--warmup", type=int, default=3, help="untimed bench steps")
     ap.add_argument("--envs", type=int, default=0, help="envs per GPU (0 = the config's: c2 4,096, c3 65,536, "
                                                          "c4 262,144)")
-    ap.add_argument("--chunk", type=int, default=0,
-                    help="env-steps per rollout launch (0 = all timed steps in one launch; with observation "
-                         "traces (c4) 0 = 50)")
+    ap.add_argument("--env-steps", "--chunk", dest="chunk", type=int, default=0,
+                    help="env-steps per env in one bench step = one rollout launch (0 = 2,000; with "
+                         "observation traces (c4) 50)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--mode", default="rollout", choices=["rollout", "step"])
@@ -162,24 +169,24 @@ def main():
     gid = np.arange(offset, offset + n, dtype=np.uint64)
     vec.reset(options={"puzzle_index": (gid * 2654435761 % len(proc)).astype(np.int64)})
 
-    K, W = args.steps, args.warmup
-    if args.chunk <= 0:
-        args.chunk = 50 if obs else K
-    chunk = max(1, min(args.chunk, K))
-    # observation traces [chunk, N, x_dim, y_dim] int32 (visited, agent_location), reused by
-    # every launch (one launch = one chunk of steps; a consumer reads them between launches)
+    K, W = max(1, args.steps), max(0, args.warmup)
+    # env-steps per env in one bench step (one launch)
+    T = 1 if args.mode == "step" else (args.chunk if args.chunk > 0 else (50 if obs else 2000))
+    chunk = T
+    # observation traces [T, N, x_dim, y_dim] int32 (visited, agent_location), reused by every
+    # launch (a consumer reads them between launches)
     X, Y = vec.x_dim, vec.y_dim
     plane_bytes = X * Y * 4
     ovis = oag = None
     if obs:
-        ovis = torch.empty((chunk, n, X, Y), dtype=torch.int32, device=dev)
+        ovis = torch.empty((T, n, X, Y), dtype=torch.int32, device=dev)
         oag = torch.empty_like(ovis)
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
-    actions = torch.randint(0, 4, (K, n), dtype=torch.uint8, device=dev, generator=g)
-    warm_actions = torch.randint(0, 4, (max(W, 1), n), dtype=torch.uint8, device=dev, generator=g)
-    rew = torch.empty((K, n), dtype=torch.int8, device=dev)
-    flags = torch.empty((K, n), dtype=torch.uint8, device=dev)
+    RA, RO = min(max(K, W), 8), min(max(K, W), 2)   # distinct action tiles / output tiles
+    actions = torch.randint(0, 4, (RA, T, n), dtype=torch.uint8, device=dev, generator=g)
+    rew = torch.empty((RO, T, n), dtype=torch.int8, device=dev)
+    flags = torch.empty((RO, T, n), dtype=torch.uint8, device=dev)
     stats = torch.zeros((n, 4), dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
 
@@ -187,40 +194,29 @@ def main():
     core = vec.core
     s_ptr = stats.data_ptr()
 
-    def run(lo, hi, acts, rew_out, flag_out, events=None):
-        if args.mode == "rollout":
-            # direct C-ABI calls on pre-validated buffers (vec.rollout() checks shapes per call)
-            ap, rp, fp = acts.data_ptr(), rew_out.data_ptr(), flag_out.data_ptr()
-            t = lo
-            while t < hi:
-                c = min(chunk, hi - t)
-                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if events is not None else None
-                if ev:
-                    ev[0].record(stream)
-                if obs:
-                    core.rollout_obs_device(c, ap + t * n, rp + t * n, fp + t * n, s_ptr, ovis.data_ptr(),
-                                            oag.data_ptr(), X, Y)
-                else:
-                    core.rollout_device(c, ap + t * n, rp + t * n, fp + t * n, s_ptr)
-                if ev:
-                    ev[1].record(stream)
-                    events.append((ev, c))
-                t += c
-        else:
-            for t in range(lo, hi):
-                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if events is not None else None
-                if ev:
-                    ev[0].record(stream)
-                core.step_device(acts.data_ptr() + t * n, rew_out.data_ptr() + t * n, flag_out.data_ptr() + t * n)
-                if ev:
-                    ev[1].record(stream)
-                    events.append((ev, 1))
+    def run(k0, k1, events=None):
+        """Bench steps k0..k1-1: direct C-ABI calls on pre-validated buffers (vec.rollout()
+        checks shapes per call), each bracketed by HIP events on the launch stream."""
+        for k in range(k0, k1):
+            ap, rp, fp = actions[k % RA].data_ptr(), rew[k % RO].data_ptr(), flags[k % RO].data_ptr()
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if events is not None else None
+            if ev:
+                ev[0].record(stream)
+            if args.mode == "step":
+                core.step_device(ap, rp, fp)
+            elif obs:
+                core.rollout_obs_device(T, ap, rp, fp, s_ptr, ovis.data_ptr(), oag.data_ptr(), X, Y)
+            else:
+                core.rollout_device(T, ap, rp, fp, s_ptr)
+            if ev:
+                ev[1].record(stream)
+                events.append((ev, T))
 
-    # warmup (untimed)
-    if W > 0:
-        wr = torch.empty((W, n), dtype=torch.int8, device=dev)
-        wf = torch.empty((W, n), dtype=torch.uint8, device=dev)
-        run(0, W, warm_actions, wr, wf)
+    # warmup (untimed), and one untimed end-of-batch gather so that RCCL's first-call setup is
+    # not inside the timed region
+    run(0, W)
+    torch.cuda.synchronize(dev)
+    sdist.gather_stats(stats)
     torch.cuda.synchronize(dev)
     stats.zero_()
     if world > 1:
@@ -228,7 +224,7 @@ def main():
     torch.cuda.synchronize(dev)
     events = []
     t0 = time.perf_counter()
-    run(0, K, actions, rew, flags, events)
+    run(W, W + K, events)
     # end-of-batch gather of per-env summaries (reward sum, dones, solved, resets): one RCCL call
     gathered = sdist.gather_stats(stats)
     torch.cuda.synchronize(dev)
@@ -242,7 +238,7 @@ def main():
     steps_per_launch = [c for _, c in events]
     avg_ms = float(np.mean(kern_ms))
     avg_T = float(np.mean(steps_per_launch))
-    value = world * n * K / elapsed
+    value = world * n * T * K / elapsed
     # algorithmic HBM bytes per launch: per env-step action 1 + reward 1 + flags 1; per env and
     # launch the state (load + store) and, for rollouts, the stats record (load + store)
     sb = state_bytes_per_env(table.words, tb)
@@ -266,7 +262,7 @@ def main():
         "n_gpus": world,
         "steps": K,
         "warmup": W,
-        "ms_per_step": round(elapsed * 1e3 / K, 6),
+        "ms_per_step": round(elapsed * 1e3 / K, 6),   # per bench step: T env-steps of every env
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -277,7 +273,8 @@ def main():
                                f"max_steps={args.max_steps}, next-step autoreset, {args.puzzles} puzzles"
                                + (f", observation='new': visited + agent_location int32 planes "
                                   f"[N, {X}, {Y}] written every step" if obs else ""),
-                   "mode": args.mode, "envs_per_gpu": n, "env_steps_per_launch": chunk if args.mode == "rollout" else 1,
+                   "mode": args.mode, "envs_per_gpu": n, "env_steps_per_bench_step": T,
+                   "env_steps_per_launch": T,
                    "parallelism": f"dp{world} (env shards, {'RCCL' if args.backend == 'nccl' else args.backend} "
                                   f"all_gather of per-env stats at end of batch)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
