@@ -562,10 +562,10 @@ struct Env<1, TB, Stack> {
         // the only legal move onto a non-free point is the traceback pop (1141-1166)
         const uint32_t pop = TB ? moved & ~__builtin_amdgcn_ubfe(w, pos, 1u) : 0u;
         const uint32_t fwd = moved ^ pop;                                            // 1167-1188
-        const uint32_t d = pos - P;                  // the neighbour's offset from e
+        const int32_t d = (int32_t)pos - (int32_t)P;  // the neighbour's offset from e
         // free board: a forward move takes the target (bit e + d + P), a pop frees the point
         // it leaves (bit e + P)
-        const uint32_t tog = e + P + (fwd ? d : 0u);
+        const uint32_t tog = e + (fwd ? pos : P);
         fr ^= (uint64_t)moved << (tog & 63u);
         if constexpr (TB) {
             const uint32_t ar = a ^ 2u;
@@ -573,7 +573,7 @@ struct Env<1, TB, Stack> {
             rl = fwd ? ar : (pop ? pnr : rl);
         }
         len = len + fwd - pop;
-        e += moved ? d : 0u;
+        e = (uint32_t)((int32_t)e + __mul24((int32_t)moved, d));   // one v_mad_i32_i24
         legal = legal_mask(P);
         const uint32_t live = rs ^ 1u;                                               // 0 on a reset step
         const uint32_t term = e == tgt ? live : 0u;                                  // 1192
@@ -596,11 +596,15 @@ struct Env<1, TB, Stack> {
     // skip it).  The branch costs ~5% with one wave per SIMD, where the unconditional gather's
     // latency is hidden anyway; with two waves per SIMD the gathers themselves are the limit
     // (MI355X, c3: 2.24e11 -> 2.94e11 env-steps/s at 131,072 envs), so the split kernel uses it.
-    template <bool COND_GATHER = false>
+    // ROOT_SET: the caller already put a reset step's trie state at the root (take_hand_word,
+    // inside its reset branch), so the per-step selects are skipped.
+    template <bool COND_GATHER = false, bool ROOT_SET = false>
     __device__ __forceinline__ int phase_trie(const Params& p) {
         // a reset step starts the new puzzle's trie at its root
-        nn = pick(s_rs != 0u, ((pflags >> 3) & 1u) << 15, nn);
-        off = pick(s_rs != 0u, ((pflags >> 1) & 1u) ^ 1u, off);
+        if constexpr (!ROOT_SET) {
+            nn = pick(s_rs != 0u, ((pflags >> 3) & 1u) << 15, nn);
+            off = pick(s_rs != 0u, ((pflags >> 1) & 1u) ^ 1u, off);
+        }
         // solution trie (first read of the record loaded at the previous step): a forward move
         // on the trie goes to the child (or leaves the trie), a pop on the trie to the parent,
         // off the trie they count the depth off it
@@ -637,25 +641,33 @@ struct Env<1, TB, Stack> {
     }
 
     // ---- k_rollout1s: the step split over a move wave (reset_next + phase_move) and a trie
-    // wave (phase_trie).  The move wave hands each step's trie inputs over as one byte:
-    // action | forward << 2 | pop << 3 | moved-with-solutions << 4 | done << 5 | reset << 6
-    __device__ __forceinline__ uint32_t hand_byte() const {
-        return (s_a & 3u) | (s_fwd << 2) | (s_pop << 3) | (s_mv << 4) | (s_done << 5) | (s_rs << 6);
+    // wave (phase_trie).  The move wave hands each step over as one 16-bit LDS word: its flag
+    // byte f (term | trunc << 1 | legal << 2 | reset << 6) | pop << 8 | forward << 9 | action
+    // << 10.  The trie wave derives done (f & 3), the reset step (bit 6) and
+    // moved-with-solutions (forward or pop, on a puzzle with solutions) from it, so the move
+    // wave's serial chain only packs three fields.  An action >= 4 never moves (forward = pop
+    // = 0); its bits above 15 are cut by the 16-bit store, and the trie wave reads only
+    // action & 3, which the cut keeps.  The I/O wave stores the low bytes as the flag output.
+    __device__ __forceinline__ uint32_t hand_word(uint32_t f) const {
+        return (((((s_a << 1) | s_fwd) << 1) | s_pop) << 8) | f;
     }
-    // the trie wave's side: unpack the byte; a reset step moves to the next puzzle's rows, as
-    // the move wave's reset_next did for its part (index + 1 mod P, SPaRC_Gym.py:1087)
+    // the trie wave's side: unpack the word; a reset step moves to the next puzzle's rows, as
+    // the move wave's reset_next did for its part (index + 1 mod P, SPaRC_Gym.py:1087), and
+    // to its trie root
     template <class Src>
-    __device__ __forceinline__ void take_hand(const Src& src, uint32_t num_puzzles, uint32_t hb) {
-        s_a = hb & 3u;
-        s_fwd = (hb >> 2) & 1u;
-        s_pop = (hb >> 3) & 1u;
-        s_mv = (hb >> 4) & 1u;
-        s_done = (hb >> 5) & 1u;
-        s_rs = hb >> 6;
-        if (s_rs) {
+    __device__ __forceinline__ void take_hand_word(const Src& src, uint32_t num_puzzles, uint32_t hw) {
+        s_rs = (hw >> 6) & 1u;
+        s_pop = TB ? (hw >> 8) & 1u : 0u;   // no pops without traceback
+        s_fwd = (hw >> 9) & 1u;
+        s_a = (hw >> 10) & 3u;
+        s_done = (uint32_t)((hw & 3u) != 0u);
+        if (s_rs) {   // the new puzzle's rows and its trie root (phase_trie<.., true>)
             pid = pid + 1 == num_puzzles ? 0u : pid + 1;
             (void)load_puzzle(src, pid);
+            nn = ((pflags >> 3) & 1u) << 15;
+            off = ((pflags >> 1) & 1u) ^ 1u;
         }
+        s_mv = (s_fwd | s_pop) & pflags & 1u;
     }
     // the trie wave's part of load(): puzzle rows, trie state and the node's record
     template <class Src>

@@ -596,8 +596,8 @@ __global__ void __launch_bounds__(kBlock1) k_rollout1(Params p, int32_t T, const
 // A lone wave issues one instruction every ~5 cycles while its SIMD can take one every ~2.5
 // from two waves, and at 65,536 envs there is exactly one 64-env wave per SIMD.  So the step is
 // cut where its data flow is one-way: a MOVE wave runs the autoreset, legality, move, path and
-// flags (reset_next + phase_move) and hands each env-step's trie inputs to a TRIE wave as one
-// LDS byte (hand_byte); the trie wave runs the solution-trie transition, the record gather and
+// flags (reset_next + phase_move) and hands each env-step's flag byte and trie inputs to a TRIE
+// wave as one 16-bit LDS word (hand_word); the trie wave runs the solution-trie transition, the record gather and
 // the reward code (phase_trie) one 16-step tile behind.  Nothing flows back: the reward code
 // never feeds the move.  The I/O wave streams action tiles in and reward / flag tiles out as in
 // k_rollout1.  Per workgroup 256 envs = 4 move waves (0-3) + 4 trie waves (4-7, on the same
@@ -610,12 +610,11 @@ __global__ void __launch_bounds__(kBlock1) k_rollout1(Params p, int32_t T, const
 constexpr int kBlock1s = 576;
 constexpr size_t kS_Act = 0;                          // actions [2 tiles][16][64]
 constexpr size_t kS_Rew = kS_Act + 2 * kTile * 64;    // reward ring [64 steps][64]
-constexpr size_t kS_Flg = kS_Rew + kRing * 64;        // flag ring [64][64]
-constexpr size_t kS_Hand = kS_Flg + kRing * 64;       // hand-over ring [64][64] (flag ring rows)
-constexpr size_t kS_Stk = kS_Hand + kRing * 64;       // move stack [64 moves][64]
+constexpr size_t kS_FH = kS_Rew + kRing * 64;         // flag | hand-over ring [64 steps][64] u16
+constexpr size_t kS_Stk = kS_FH + 2 * kRing * 64;     // move stack [64 moves][64]
 constexpr size_t kS_Pair = kS_Stk + 64 * 64;          // per move / trie wave pair
-constexpr size_t kS_Fin = 4 * kS_Pair;                // trie wave's final state [4][64] uint4
-constexpr size_t kS_Base = kS_Fin + 4 * 64 * sizeof(uint4);
+constexpr size_t kS_Fin = 4 * kS_Pair;                // trie wave's final state [4][64] 2 x uint4
+constexpr size_t kS_Base = kS_Fin + 4 * 64 * 2 * sizeof(uint4);
 
 template <bool TB, bool RAND, bool LDS_TABLE>
 __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, const uint8_t* __restrict__ act,
@@ -662,7 +661,17 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
                     const uint8_t* base = smem + w * kS_Pair + row * 64 + (c8 & 63u);
                     const size_t o = (size_t)(k * kTile + h * 8 + r8) * n + wg_base + q * 128 + c8;
                     if (rew) nt_store16(reinterpret_cast<uint8_t*>(rew) + o, *reinterpret_cast<const u32x4*>(base + kS_Rew));
-                    if (flg) nt_store16(flg + o, *reinterpret_cast<const u32x4*>(base + kS_Flg));
+                    if (flg) {   // the low bytes of 16 u16 ring entries (flag | hand-over << 8)
+                        const uint8_t* fh = smem + w * kS_Pair + kS_FH + row * 128 + 2 * (c8 & 63u);
+                        const u32x4 a = *reinterpret_cast<const u32x4*>(fh);
+                        const u32x4 b = *reinterpret_cast<const u32x4*>(fh + 16);
+                        u32x4 v;
+                        v.x = __builtin_amdgcn_perm(a.y, a.x, 0x06040200u);
+                        v.y = __builtin_amdgcn_perm(a.w, a.z, 0x06040200u);
+                        v.z = __builtin_amdgcn_perm(b.y, b.x, 0x06040200u);
+                        v.w = __builtin_amdgcn_perm(b.w, b.z, 0x06040200u);
+                        nt_store16(flg + o, v);
+                    }
                 }
             }
         };
@@ -681,15 +690,17 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
     const uint32_t pr = wv & 3u;                                 // the pair's 64 envs
     const uint32_t i = wg_base + pr * 64u + lane;
     uint8_t* pb = smem + pr * kS_Pair;
-    uint4* fin = reinterpret_cast<uint4*>(smem + kS_Fin) + pr * 64u + lane;
+    uint4* fin = reinterpret_cast<uint4*>(smem + kS_Fin) + 2u * (pr * 64u + lane);
     using Stack = typename std::conditional<TB, LdsStack<64>, RegStack>::type;
     Env<1, TB, Stack> e;
     if (wv < 4) {                                                // ---- move waves
         if constexpr (TB) e.stk.col = pb + kS_Stk + lane;
         e.load(p, src, i);
         const uint64_t gid = p.env_offset + i;
-        uint8_t* tf = pb + kS_Flg + lane;
-        int acc_y = 0, acc_w = 0;
+        uint16_t* tf = reinterpret_cast<uint16_t*>(pb + kS_FH) + lane;
+        // done / reset counts: with traceback the move wave is the longer chain and the trie
+        // wave counts them (from the hand-over word); without, the move wave counts them
+        uint32_t acc_y = 0, acc_w = 0;
         __syncthreads();                                         // B_0
         for (int32_t k = 0; k < K; ++k) {
             const uint8_t* ta = pb + kS_Act + (k & 1) * (kTile * 64) + lane;
@@ -710,27 +721,29 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
                     const uint32_t row = (uint32_t)(k * kTile + g + j) & (kRing - 1);
                     e.reset_next(p, src);
                     const uint32_t f = e.phase_move(p, av[j]);
-                    tf[row * 64] = (uint8_t)f;
-                    tf[row * 64 + (kS_Hand - kS_Flg)] = (uint8_t)e.hand_byte();
-                    acc_y += (int)e.pending;
-                    acc_w += (int)e.s_rs;
+                    tf[row * 64] = (uint16_t)e.hand_word(f);
+                    if constexpr (!TB) {
+                        acc_y += e.pending;
+                        acc_w += e.s_rs;
+                    }
                 }
             }
             __syncthreads();                                     // B_{k+1}
         }
         __syncthreads();                                         // B_{K+1}
         __syncthreads();                                         // B_{K+2}: the trie state is in fin
-        const uint4 fs = *fin;
+        const uint4 fs = fin[0];
         e.nn = fs.x & 0xFFFFu;
         e.outcome = fs.x >> 16;
         e.off = fs.y;
         e.store(p, src, i);
         if (stats) {
+            const uint4 fc = fin[1];
             int4 st = stats[i];
             st.x += (int)fs.z;
-            st.y += acc_y;
+            st.y += (int)(fc.x + acc_y);
             st.z += (int)fs.w;
-            st.w += acc_w;
+            st.w += (int)(fc.y + acc_w);
             stats[i] = st;
         }
     } else {                                                     // ---- trie waves
@@ -741,10 +754,10 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         __builtin_amdgcn_s_setprio(1);
 #endif
         e.load_trie(p, src, i);
-        const uint8_t* th = pb + kS_Hand + lane;
+        const uint16_t* th = reinterpret_cast<const uint16_t*>(pb + kS_FH) + lane;
         uint8_t* tr = pb + kS_Rew + lane;
         int acc_x = 0;
-        uint32_t acc_z = 0;
+        uint32_t acc_z = 0, acc_y = 0, acc_w = 0;
         __syncthreads();                                         // B_0
         __syncthreads();                                         // B_1 (interval 0: no tile yet)
         for (int32_t k = 1; k <= K; ++k) {
@@ -756,23 +769,28 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
 #endif
 #pragma unroll 1
             for (int g = 0; g < kTile; g += 4) {
-                // the group's 4 hand-over bytes first (one LDS wait), then its 4 steps
+                // the group's 4 flag | hand-over words first (one LDS wait), then its 4 steps
                 const uint32_t row0 = (uint32_t)((k - 1) * kTile + g) & (kRing - 1);
                 uint32_t hb[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) hb[j] = th[(row0 + j) * 64];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    e.take_hand(src, p.tab.num_puzzles, hb[j]);
-                    const int code = e.template phase_trie<true>(p);
+                    e.take_hand_word(src, p.tab.num_puzzles, hb[j]);
+                    const int code = e.template phase_trie<true, true>(p);
                     tr[(row0 + j) * 64] = (uint8_t)code;
                     acc_x += code;
                     acc_z += e.solved;
+                    if constexpr (TB) {
+                        acc_y += e.s_done;
+                        acc_w += e.s_rs;
+                    }
                 }
             }
             __syncthreads();                                     // B_{k+1}
         }
-        *fin = make_uint4(e.nn | (e.outcome << 16), e.off, (uint32_t)acc_x, acc_z);
+        fin[0] = make_uint4(e.nn | (e.outcome << 16), e.off, (uint32_t)acc_x, acc_z);
+        fin[1] = make_uint4(acc_y, acc_w, 0u, 0u);
         __syncthreads();                                         // B_{K+2}
     }
 }
