@@ -466,8 +466,9 @@ struct Env<1, TB, Stack> {
     // _get_legal_actions (1024-1051): bit d = direction d is legal; sets the window w
     __device__ __forceinline__ uint32_t legal_mask(uint32_t P) {
         w = (uint32_t)(fr >> (e & 63u));
-        const uint32_t ud = __builtin_amdgcn_ubfe(w, P - 1u, 3u);   // up, self, down
-        uint32_t m = ((ud & 5u) << 1) | __builtin_amdgcn_ubfe(w, 2u * P, 1u) | ((w << 2) & 4u);
+        // bits P-2..P+1 of w: (-, up, self, down); up and down land on their action bits 1, 3
+        const uint32_t ud = __builtin_amdgcn_ubfe(w, P - 2u, 4u);
+        uint32_t m = (ud & 10u) | (((w << 2) & 4u) | __builtin_amdgcn_ubfe(w, 2u * P, 1u));
         // traceback: path[-2] (the reverse of the last move) is visited but legal
         if constexpr (TB) m |= ((len + bk) >> 31) << rl;
         return m;

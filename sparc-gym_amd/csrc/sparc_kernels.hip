@@ -753,6 +753,9 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         // 1,000 steps; priority to the move wave instead: no change)
         __builtin_amdgcn_s_setprio(1);
 #endif
+#ifdef SPARC_DIAG_TRIE_FROM_LDS
+        e.diag_lds = smem + kS_Base;
+#endif
         e.load_trie(p, src, i);
         const uint16_t* th = reinterpret_cast<const uint16_t*>(pb + kS_FH) + lane;
         uint8_t* tr = pb + kS_Rew + lane;
