@@ -455,6 +455,9 @@ struct Env<1, TB, Stack> {
     // solutions, done, reset step
     uint32_t s_a = 0, s_fwd = 0, s_pop = 0, s_mv = 0, s_done = 0, s_rs = 0;
     uint4 rec;
+    // k_rollout1s trie wave: the next puzzle's index and row (take_hand_word_pf)
+    uint4 nx;
+    uint32_t npid = 0;
 
     // all arms are computed unconditionally and merged with masks: a C++ ?: whose arms are
     // 64-bit shifts is otherwise lowered to exec-masked if/else blocks
@@ -478,7 +481,9 @@ struct Env<1, TB, Stack> {
     // solutions, bit1 root valid, bit2 start closed, bit3 root terminal
     template <class Src>
     __device__ __forceinline__ uint32_t load_puzzle(const Src& src, uint32_t q) {
-        const uint4 r = src.get_row1(q);
+        return apply_row(src.get_row1(q));
+    }
+    __device__ __forceinline__ uint32_t apply_row(const uint4 r) {
         tgt = (r.x >> 8) & 0xFFu;
         pflags = r.x >> 16;
         trie_base = r.y;
@@ -670,6 +675,38 @@ struct Env<1, TB, Stack> {
         }
         s_mv = (s_fwd | s_pop) & pflags & 1u;
     }
+    // ---- k_rollout1s trie wave without traceback: the next puzzle's row (the autoreset
+    // always loads pid + 1 mod P, SPaRC_Gym.py:1087) is read from LDS one step ahead, every
+    // step, into nx, so that a reset step applies registers instead of waiting on an LDS read
+    // (a 64-lane wave has a resetting lane on most steps).  npid = the puzzle after pid.
+    // MI355X, 2,000-step launches: c2 pool 0.453 -> 0.435 ms at 65,536 envs and 0.412 ->
+    // 0.398 ms at 4,096; with traceback (c3) 0.472 -> 0.478 ms, so TB keeps take_hand_word.
+    // The same prefetch in the move wave was slower for both.
+    __device__ __forceinline__ static uint32_t next_pid(uint32_t q, uint32_t num_puzzles) {
+        return q + 1 == num_puzzles ? 0u : q + 1;
+    }
+    template <class Src>
+    __device__ __forceinline__ void prefetch_trie(const Src& src) {
+        nx = src.get_row1(npid);
+    }
+    template <class Src>
+    __device__ __forceinline__ void take_hand_word_pf(const Src& src, uint32_t num_puzzles, uint32_t hw) {
+        s_rs = (hw >> 6) & 1u;
+        s_pop = TB ? (hw >> 8) & 1u : 0u;
+        s_fwd = (hw >> 9) & 1u;
+        s_a = (hw >> 10) & 3u;
+        s_done = (uint32_t)((hw & 3u) != 0u);
+        if (s_rs) {
+            pid = npid;
+            npid = next_pid(npid, num_puzzles);
+            (void)apply_row(nx);
+            nn = ((pflags >> 3) & 1u) << 15;
+            off = ((pflags >> 1) & 1u) ^ 1u;
+        }
+        prefetch_trie(src);
+        s_mv = (s_fwd | s_pop) & pflags & 1u;
+    }
+
     // the trie wave's part of load(): puzzle rows, trie state and the node's record
     template <class Src>
     __device__ __forceinline__ void load_trie(const Params& p, const Src& src, uint32_t i) {

@@ -757,6 +757,10 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         e.diag_lds = smem + kS_Base;
 #endif
         e.load_trie(p, src, i);
+        if constexpr (!TB) {
+            e.npid = e.next_pid(e.pid, p.tab.num_puzzles);
+            e.prefetch_trie(src);
+        }
         const uint16_t* th = reinterpret_cast<const uint16_t*>(pb + kS_FH) + lane;
         uint8_t* tr = pb + kS_Rew + lane;
         int acc_x = 0;
@@ -779,7 +783,8 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
                 for (int j = 0; j < 4; ++j) hb[j] = th[(row0 + j) * 64];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    e.take_hand_word(src, p.tab.num_puzzles, hb[j]);
+                    if constexpr (TB) e.take_hand_word(src, p.tab.num_puzzles, hb[j]);
+                    else e.take_hand_word_pf(src, p.tab.num_puzzles, hb[j]);
                     const int code = e.template phase_trie<true, true>(p);
                     tr[(row0 + j) * 64] = (uint8_t)code;
                     acc_x += code;
