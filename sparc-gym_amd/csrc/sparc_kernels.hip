@@ -597,17 +597,18 @@ __global__ void __launch_bounds__(kBlock1) k_rollout1(Params p, int32_t T, const
 // from two waves, and at 65,536 envs there is exactly one 64-env wave per SIMD.  So the step is
 // cut where its data flow is one-way: a MOVE wave runs the autoreset, legality, move, path and
 // flags (reset_next + phase_move) and hands each env-step's flag byte and trie inputs to a TRIE
-// wave as one 16-bit LDS word (hand_word); the trie wave runs the solution-trie transition, the record gather and
-// the reward code (phase_trie) one 16-step tile behind.  Nothing flows back: the reward code
-// never feeds the move.  The I/O wave streams action tiles in and reward / flag tiles out as in
-// k_rollout1.  Per workgroup 256 envs = 4 move waves (0-3) + 4 trie waves (4-7, on the same
-// SIMDs as the move waves of their envs) + 1 I/O wave; one barrier per tile:
+// wave as one 16-bit LDS word (hand_word); the trie wave runs the solution-trie transition,
+// the record gather and the reward code (phase_trie) one 16-step tile behind.  Nothing flows
+// back: the reward code never feeds the move.  I/O waves stream action tiles in and reward /
+// flag tiles out as in k_rollout1.  Per workgroup 256 envs = 4 move waves (0-3) + 4 trie waves
+// (4-7, on the same SIMDs as the move waves of their envs) + 4 I/O waves (8-11, one per SIMD);
+// one barrier per tile:
 //   interval k (between barriers B_k and B_k+1): move waves step tile k; trie waves finish
-//   tile k-1; the I/O wave loads the actions of tile k+1 and stores the outputs of tile k-2.
+//   tile k-1; the I/O waves load the actions of tile k+1 and store the outputs of tile k-2.
 // Only full workgroups, T % 16 == 0 and 16-B aligned I/O; the host runs any tail through
 // k_rollout1.  The state after the launch is the same SoA record (the trie wave hands its
 // final node / depth / outcome and stats to the move wave through LDS before the store).
-constexpr int kBlock1s = 576;
+constexpr int kBlock1s = 768;
 constexpr size_t kS_Act = 0;                          // actions [2 tiles][16][64]
 constexpr size_t kS_Rew = kS_Act + 2 * kTile * 64;    // reward ring [64 steps][64]
 constexpr size_t kS_FH = kS_Rew + kRing * 64;         // flag | hand-over ring [64 steps][64] u16
@@ -638,26 +639,26 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
     const uint32_t wg_base = blockIdx.x * 256u;
     const int32_t K = T / kTile;
 
-    if (wv == 8) {                                               // ---- the I/O wave
+    if (wv >= 8) {                                               // ---- the I/O waves
+        // one per SIMD (waves 8-11), each a quarter of the streamed traffic: I/O wave j loads
+        // the action tile of pair j and stores rows 8 * (j >> 1) .. + 7 of env half j & 1 of
+        // the output tiles (whole 128-B lines).  With one I/O wave for all four pairs its
+        // issue load sat on one SIMD (MI355X, c3: 0.468 -> 0.466 ms per launch with four)
+        const uint32_t io = wv - 8u;
         const uint32_t r = lane >> 2, c = (lane & 3u) * 16u;
         auto load_tile = [&](int32_t k) {                        // actions of tile k -> buffer k & 1
             if constexpr (!RAND) {
-                u32x4 v[4];
-#pragma unroll
-                for (int w = 0; w < 4; ++w) v[w] = nt_load16(act + (size_t)(k * kTile + r) * n + wg_base + w * 64 + c);
-#pragma unroll
-                for (int w = 0; w < 4; ++w)
-                    *reinterpret_cast<u32x4*>(smem + w * kS_Pair + kS_Act + (k & 1) * (kTile * 64) + r * 64 + c) = v[w];
+                const u32x4 v = nt_load16(act + (size_t)(k * kTile + r) * n + wg_base + io * 64 + c);
+                *reinterpret_cast<u32x4*>(smem + io * kS_Pair + kS_Act + (k & 1) * (kTile * 64) + r * 64 + c) = v;
             }
         };
         auto store_tile = [&](int32_t k) {                       // whole 128-B lines, as k_rollout1
             const uint32_t r8 = lane >> 3, c8 = (lane & 7u) * 16u;
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
+            {
+                const uint32_t h = io >> 1, q = io & 1u;
                 const uint32_t row = (uint32_t)((k * kTile) & (kRing - 1)) + h * 8 + r8;
-#pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    const int w = 2 * q + (int)(c8 >> 6);
+                {
+                    const uint32_t w = 2 * q + (c8 >> 6);
                     const uint8_t* base = smem + w * kS_Pair + row * 64 + (c8 & 63u);
                     const size_t o = (size_t)(k * kTile + h * 8 + r8) * n + wg_base + q * 128 + c8;
                     if (rew) nt_store16(reinterpret_cast<uint8_t*>(rew) + o, *reinterpret_cast<const u32x4*>(base + kS_Rew));
@@ -678,11 +679,17 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         if (K > 0) load_tile(0);
         __syncthreads();                                         // B_0
         for (int32_t k = 0; k <= K; ++k) {
+#ifdef SPARC_DIAG_SPLIT_IO_IDLE   // timing only: two action tiles reused, no output stores
+            if (k + 1 < K && k < 1) load_tile(k + 1);
+#else
             if (k + 1 < K) load_tile(k + 1);
             if (k >= 2) store_tile(k - 2);
+#endif
             __syncthreads();                                     // B_{k+1}
         }
+#ifndef SPARC_DIAG_SPLIT_IO_IDLE
         if (K >= 1) store_tile(K - 1);
+#endif
         __syncthreads();                                         // B_{K+2}
         return;
     }
