@@ -160,6 +160,22 @@ int sparc_step_obs_device(void *ctx, const uint8_t *d_actions, int8_t *d_reward,
                           int32_t *d_visited, int32_t *d_agent, int32_t x_dim, int32_t y_dim,
                           uint32_t *d_puzzle, uint32_t *d_xy);
 
+/* One gymnasium vector step in ONE launch (SPaRCVecEnv.step; SPaRC_Gym.step 1111-1238 for every
+ * env): the step and its 'new' planes as sparc_step_obs_device, plus the gym outputs the host
+ * would otherwise derive with separate launches:
+ *   d_actions: [N] elements of action_bytes = 1 (uint8; >= 4 is illegal = no move), 4 (int32)
+ *              or 8 (int64; < 0 or >= 4 is illegal), so a caller's int64 actions need no cast;
+ *   d_reward [N] double = reward code / 100 (the reference's exact float64 values -1, -0.01,
+ *   0, 0.01, 1); d_terminated / d_truncated / d_autoreset [N] 0/1 bytes (bool tensors);
+ *   d_legal [N] = the legal-action mask of the new state (bit a = action a, 1024-1051);
+ *   d_loc [N][2] int32 = the agent's (x, y).
+ * Every output pointer may be NULL (not written).  x_dim * y_dim <= 256 when planes are given.
+ * Device pointers, asynchronous. */
+int sparc_step_gym_device(void *ctx, const void *d_actions, int32_t action_bytes, double *d_reward,
+                          uint8_t *d_terminated, uint8_t *d_truncated, uint8_t *d_legal, uint8_t *d_autoreset,
+                          int8_t *d_reward_code, uint8_t *d_flags, int32_t *d_visited, int32_t *d_agent,
+                          int32_t x_dim, int32_t y_dim, uint32_t *d_puzzle, int32_t *d_loc);
+
 /* sparc_rollout_device that also records the 'new' observation after every step: planes
  * [T][N][x_dim][y_dim] int32 (visited / agent_location; either may be NULL), so step t's
  * entries equal sparc_step_obs_device's after the t-th of T single steps.  Every store is a

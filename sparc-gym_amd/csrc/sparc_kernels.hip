@@ -190,12 +190,30 @@ __device__ __forceinline__ void obs_emit(ObsWave<W>* ow, const uint16_t* lut, ui
 
 // step() + the 'new' observation in one launch (SPaRCVecEnv.step): the gym one-call-per-step
 // contract with the planes, the puzzle index and the agent (x | y << 8) of every env
+// the gym outputs of sparc_step_gym_device (each pointer may be null) and the action width
+struct GymOut {
+    const void* act;      // [N] uint8 (>= 4 illegal), int32 or int64 (< 0 or >= 4 illegal)
+    uint32_t abytes;      // 1, 4 or 8
+    double* r64;          // reward code / 100
+    uint8_t* term;
+    uint8_t* trunc;
+    uint8_t* legal;
+    uint8_t* areset;
+    int32_t* loc;         // [N][2] (x, y)
+};
+
+__device__ __forceinline__ uint32_t read_action(const GymOut& g, uint32_t i) {
+    if (g.abytes == 1) return static_cast<const uint8_t*>(g.act)[i];
+    const int64_t v = g.abytes == 4 ? (int64_t) static_cast<const int32_t*>(g.act)[i]
+                                    : static_cast<const int64_t*>(g.act)[i];
+    return (v >= 0 && v < 4) ? (uint32_t)v : 255u;
+}
+
 template <int W, bool TB>
-__global__ void __launch_bounds__(kBlock) k_step_obs(Params p, const uint8_t* __restrict__ act,
-                                                     int8_t* __restrict__ rew, uint8_t* __restrict__ flg,
-                                                     int32_t* __restrict__ vout, int32_t* __restrict__ aout,
-                                                     uint32_t XD, uint32_t YD, uint32_t* __restrict__ pidx,
-                                                     uint32_t* __restrict__ xy) {
+__global__ void __launch_bounds__(kBlock) k_step_obs(Params p, GymOut g, int8_t* __restrict__ rew,
+                                                     uint8_t* __restrict__ flg, int32_t* __restrict__ vout,
+                                                     int32_t* __restrict__ aout, uint32_t XD, uint32_t YD,
+                                                     uint32_t* __restrict__ pidx, uint32_t* __restrict__ xy) {
     __shared__ ObsWave<W> ow[kWaves];
     __shared__ uint16_t lut[kObsCells];
     obs_build_lut(lut, XD, YD, p.pitch, W, threadIdx.x, kBlock);
@@ -213,13 +231,23 @@ __global__ void __launch_bounds__(kBlock) k_step_obs(Params p, const uint8_t* __
     if (active) {
         e.load(p, src, i);
         uint32_t f;
-        const int c = e.advance(p, src, act[i], f);
+        const int c = e.advance(p, src, read_action(g, i), f);
         e.store(p, src, i);
-        rew[i] = (int8_t)c;
-        flg[i] = (uint8_t)f;
+        if (rew) rew[i] = (int8_t)c;
+        if (flg) flg[i] = (uint8_t)f;
+        // reward code / 100 in float64: the reference's exact values (REWARD_SCALE in vec_env)
+        if (g.r64) g.r64[i] = (double)c / 100.0;
+        if (g.term) g.term[i] = (uint8_t)(f & 1u);
+        if (g.trunc) g.trunc[i] = (uint8_t)((f >> 1) & 1u);
+        if (g.legal) g.legal[i] = (uint8_t)((f >> 2) & 15u);
+        if (g.areset) g.areset[i] = (uint8_t)((f >> 6) & 1u);
         e.obs_words(p, src, v, ab);
         if (pidx) pidx[i] = e.pid;
-        if (xy) xy[i] = e.agent_xy(p);
+        if (xy || g.loc) {
+            const uint32_t a = e.agent_xy(p);
+            if (xy) xy[i] = a;
+            if (g.loc) reinterpret_cast<int2*>(g.loc)[i] = make_int2((int)(a & 0xFFu), (int)((a >> 8) & 0xFFu));
+        }
     }
     const uint32_t XY = XD * YD, cnt = p.n - wave_base < 64u ? p.n - wave_base : 64u;
     const size_t run = (size_t)wave_base * XY;
@@ -1405,9 +1433,35 @@ int sparc_step_obs_device(void* ctx, const uint8_t* d_act, int8_t* d_rew, uint8_
     rc = check_obs_dims(c, x_dim, y_dim);
     if (rc) return rc;
     const Params p = make_params(c);
+    const GymOut g{d_act, 1u, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     dispatch_w_tb(c->W, c->cfg.traceback, [&](auto w, auto tb) {
         k_step_obs<decltype(w)::value, decltype(tb)::value><<<grid_for(c->n), kBlock, 0, c->stream>>>(
-            p, d_act, d_rew, d_flags, d_visited, d_agent, (uint32_t)x_dim, (uint32_t)y_dim, d_puzzle, d_xy);
+            p, g, d_rew, d_flags, d_visited, d_agent, (uint32_t)x_dim, (uint32_t)y_dim, d_puzzle, d_xy);
+    });
+    return launch_check(c);
+}
+
+int sparc_step_gym_device(void* ctx, const void* d_act, int32_t action_bytes, double* d_reward, uint8_t* d_term,
+                          uint8_t* d_trunc, uint8_t* d_legal, uint8_t* d_areset, int8_t* d_rew_code,
+                          uint8_t* d_flags, int32_t* d_visited, int32_t* d_agent, int32_t x_dim, int32_t y_dim,
+                          uint32_t* d_puzzle, int32_t* d_loc) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    int rc = check_ctx(c, true);
+    if (rc) return rc;
+    if (!d_act) return fail(c, SPARC_E_INVALID, "null actions");
+    if (action_bytes != 1 && action_bytes != 4 && action_bytes != 8)
+        return fail(c, SPARC_E_INVALID, "action_bytes must be 1, 4 or 8");
+    if (d_visited || d_agent) {
+        rc = check_obs_dims(c, x_dim, y_dim);
+        if (rc) return rc;
+    } else {
+        x_dim = y_dim = 1;
+    }
+    const Params p = make_params(c);
+    const GymOut g{d_act, (uint32_t)action_bytes, d_reward, d_term, d_trunc, d_legal, d_areset, d_loc};
+    dispatch_w_tb(c->W, c->cfg.traceback, [&](auto w, auto tb) {
+        k_step_obs<decltype(w)::value, decltype(tb)::value><<<grid_for(c->n), kBlock, 0, c->stream>>>(
+            p, g, d_rew_code, d_flags, d_visited, d_agent, (uint32_t)x_dim, (uint32_t)y_dim, d_puzzle, nullptr);
     });
     return launch_check(c);
 }

@@ -57,6 +57,9 @@ _SIGS = {
     "sparc_obs_pack_device": ([c_void_p, c_void_p, c_void_p, c_int32, c_int32], c_int32),
     "sparc_step_obs_device": ([c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32,
                                c_void_p, c_void_p], c_int32),
+    "sparc_step_gym_device": ([c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                               c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p],
+                              c_int32),
     "sparc_rollout_obs_device": ([c_void_p, c_int32, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_int32, c_int32], c_int32),
     "sparc_read_state": ([c_void_p, ctypes.POINTER(SparcStateHost)], c_int32),

@@ -149,6 +149,13 @@ class SparcCore:
         self._check(self.lib.sparc_step_obs_device(self.ctx, d_actions, d_reward, d_flags, d_visited, d_agent,
                                                    int(x_dim), int(y_dim), d_puzzle, d_xy))
 
+    def step_gym_device(self, d_actions, action_bytes, d_reward=None, d_terminated=None, d_truncated=None,
+                        d_legal=None, d_autoreset=None, d_reward_code=None, d_flags=None, d_visited=None,
+                        d_agent=None, x_dim=1, y_dim=1, d_puzzle=None, d_loc=None):
+        self._check(self.lib.sparc_step_gym_device(self.ctx, d_actions, int(action_bytes), d_reward, d_terminated,
+                                                   d_truncated, d_legal, d_autoreset, d_reward_code, d_flags,
+                                                   d_visited, d_agent, int(x_dim), int(y_dim), d_puzzle, d_loc))
+
     def rollout_obs_device(self, T, d_actions, d_reward, d_flags, d_stats, d_visited, d_agent, x_dim, y_dim,
                            seed=0, t0=0):
         self._check(self.lib.sparc_rollout_obs_device(self.ctx, int(T), d_actions, int(seed) & (2**64 - 1),

@@ -66,6 +66,7 @@ class SPaRCVecEnv:
         self._flags = torch.empty(n, dtype=torch.uint8, device=dev)
         self._pidx = torch.empty(n, dtype=torch.int32, device=dev)
         self._pos = torch.empty(n, dtype=torch.int32, device=dev)
+        self._loc = torch.empty((n, 2), dtype=torch.int32, device=dev)
         if observation == "new":
             self._vis = torch.empty((n, self.x_dim, self.y_dim), dtype=torch.int32, device=dev)
             self._agent = torch.empty_like(self._vis)
@@ -114,6 +115,13 @@ class SPaRCVecEnv:
         if self.observation == "new":
             self.core.obs_pack_device(self._vis.data_ptr(), self._agent.data_ptr(), self.x_dim, self.y_dim)
         return self._obs_dict()
+
+    def _step_obs_dict(self):
+        """_obs_dict after step_gym_device, which wrote the agent's (x, y) into _loc itself."""
+        if self.observation == "compact":
+            return {"puzzle_index": self._pidx, "agent_location": self._loc}
+        return {"visited": self._vis, "agent_location": self._agent, "puzzle_index": self._pidx,
+                "agent_xy": self._loc}
 
     def _obs_dict(self):
         loc = torch.stack([self._pos & 0xFF, (self._pos >> 8) & 0xFF], dim=1)
@@ -179,29 +187,40 @@ class SPaRCVecEnv:
         return self._obs(), info
 
     def step(self, actions):
-        """One step() of every env: actions [N] (int; >= 4 is illegal = no move)."""
-        s = self._stream()
+        """One step() of every env: actions [N] (uint8: >= 4 is illegal = no move; other integer
+        types: < 0 or >= 4 is illegal).  ONE launch (sparc_step_gym_device) writes the step, the
+        post-step observation and the gym outputs: reward [N] float64 (the reference's exact
+        values), terminated / truncated [N] bool, and info's legal_mask, autoreset and
+        reward_code.  reward / terminated / truncated / legal_mask / autoreset are fresh
+        tensors per call; the observation tensors and reward_code are the env's buffers,
+        overwritten by the next step (the reference returns its planes by reference too)."""
+        self._stream()
+        n = self.num_envs
         a = torch.as_tensor(actions, device=self.device)
-        if a.shape != (self.num_envs,):
-            raise ValueError(f"actions must have shape ({self.num_envs},)")
-        if a.dtype != torch.uint8:
-            a = torch.where((a >= 0) & (a < 4), a, torch.full_like(a, 255)).to(torch.uint8)
-        with torch.cuda.stream(s):
-            self._act.copy_(a)
-        # one launch: step + the post-step observation (k_step_obs)
+        if a.shape != (n,):
+            raise ValueError(f"actions must have shape ({n},)")
+        if a.dtype not in (torch.uint8, torch.int32, torch.int64):
+            if a.dtype.is_floating_point or a.dtype == torch.bool:
+                raise ValueError("actions must be integers")
+            a = a.to(torch.int64)
+        a = a.contiguous()
+        # one allocation for the fresh outputs: reward f64 [N] | terminated | truncated | legal | autoreset
+        buf = torch.empty(12 * n, dtype=torch.uint8, device=self.device)
+        reward = buf[:8 * n].view(torch.float64)
+        terminated = buf[8 * n:9 * n].view(torch.bool)
+        truncated = buf[9 * n:10 * n].view(torch.bool)
+        legal = buf[10 * n:11 * n]
+        autoreset = buf[11 * n:].view(torch.bool)
         new = self.observation == "new"
-        self.core.step_obs_device(self._act.data_ptr(), self._rew.data_ptr(), self._flags.data_ptr(),
-                                  self._vis.data_ptr() if new else None, self._agent.data_ptr() if new else None,
-                                  self.x_dim if new else 1, self.y_dim if new else 1,
-                                  self._pidx.data_ptr(), self._pos.data_ptr())
-        f = self._flags
-        reward = self._rew.to(torch.float64) / REWARD_SCALE
-        terminated = (f & 1).bool()
-        truncated = (f & 2).bool()
-        info = {"legal_mask": (f >> 2) & 0xF, "autoreset": (f & 64).bool(), "reward_code": self._rew}
+        self.core.step_gym_device(a.data_ptr(), a.element_size(), reward.data_ptr(), terminated.data_ptr(),
+                                  truncated.data_ptr(), legal.data_ptr(), autoreset.data_ptr(), self._rew.data_ptr(),
+                                  self._flags.data_ptr(), self._vis.data_ptr() if new else None,
+                                  self._agent.data_ptr() if new else None, self.x_dim if new else 1,
+                                  self.y_dim if new else 1, self._pidx.data_ptr(), self._loc.data_ptr())
+        info = {"legal_mask": legal, "autoreset": autoreset, "reward_code": self._rew}
         if self.rules:
             info["rule_bits"] = self.rule_audit()["bits"]
-        return self._obs_dict(), reward, terminated, truncated, info
+        return self._step_obs_dict(), reward, terminated, truncated, info
 
     def rollout(self, T, actions=None, seed=0, t0=0, stats=None, record=True, out=None, obs=False, obs_out=None):
         """T steps of every env in ONE kernel launch.  actions: [T, N] uint8 on the GPU or None

@@ -439,3 +439,51 @@ def test_obs_entry_points_validate_plane_dims(on_gpu):
     torch.cuda.synchronize()
     vis = planes[:n * 49].view(n, 7, 7).cpu().numpy()
     assert vis.reshape(n, -1).sum(1).min() >= 1          # the start (and any move) is visited
+
+
+def test_step_gym_action_types_and_outputs(on_gpu):
+    """SPaRCVecEnv.step's one-launch gym outputs (sparc_step_gym_device): int64, int32 and uint8
+    actions with out-of-range values give identical steps (< 0 or >= 4 is illegal for the
+    integer types, >= 4 for uint8); reward == reward_code / 100 in float64, terminated /
+    truncated / legal_mask / autoreset equal the flag bits; agent_xy equals the reset path's
+    (x, y); compact and 'new' observations agree.  Also checks the ABI's argument validation."""
+    from sparc_gym_amd import SPaRCVecEnv
+    proc, table = _make("7x7_full", seed=21)
+    n, T = 1000, 60
+    rng = np.random.default_rng(5)
+    acts = rng.integers(-3, 7, size=(T, n)).astype(np.int64)
+    envs = {k: SPaRCVecEnv(n, processed=proc, table=table, traceback=True, max_steps=25,
+                           observation="new" if k != "compact" else "compact")
+            for k in ("i64", "i32", "u8", "compact")}
+    for v in envs.values():
+        v.reset(seed=3)
+    for t in range(T):
+        a64 = torch.from_numpy(acts[t]).cuda()
+        outs = {"i64": envs["i64"].step(a64), "i32": envs["i32"].step(a64.to(torch.int32)),
+                "u8": envs["u8"].step(torch.where((a64 >= 0) & (a64 < 4), a64, 255).to(torch.uint8)),
+                "compact": envs["compact"].step(acts[t])}                      # numpy int64
+        ref_obs, ref_r, ref_te, ref_tr, ref_info = outs["i64"]
+        code = ref_info["reward_code"].to(torch.float64) / 100.0
+        assert torch.equal(ref_r, code)
+        assert ref_r.dtype == torch.float64 and ref_te.dtype == torch.bool and ref_tr.dtype == torch.bool
+        for k, (obs, r, te, tr, info) in outs.items():
+            assert torch.equal(r, ref_r) and torch.equal(te, ref_te) and torch.equal(tr, ref_tr), (k, t)
+            assert torch.equal(info["legal_mask"], ref_info["legal_mask"]), (k, t)
+            assert torch.equal(info["autoreset"], ref_info["autoreset"]), (k, t)
+            assert torch.equal(obs["puzzle_index"], ref_obs["puzzle_index"]), (k, t)
+            loc = obs["agent_location"] if k == "compact" else obs["agent_xy"]
+            assert torch.equal(loc, ref_obs["agent_xy"]), (k, t)
+            if k != "compact":
+                assert torch.equal(obs["visited"], ref_obs["visited"]), (k, t)
+        f = envs["i64"]._flags
+        assert torch.equal(ref_te, (f & 1).bool()) and torch.equal(ref_tr, (f & 2).bool())
+        assert torch.equal(ref_info["legal_mask"], (f >> 2) & 0xF)
+        assert torch.equal(ref_info["autoreset"], (f & 64).bool())
+    # the step path's (x, y) equals the observation-pack path's (reset's _obs)
+    v = envs["compact"]
+    step_xy = v._loc.clone()
+    assert torch.equal(v._obs()["agent_location"], step_xy)
+    with pytest.raises(ValueError):
+        v.step(torch.zeros(n, dtype=torch.float32))
+    with pytest.raises(ValueError):
+        v.core.step_gym_device(torch.zeros(n, dtype=torch.int16, device="cuda").data_ptr(), 2)
