@@ -116,6 +116,26 @@ class SPaRCVecEnv:
             self.core.obs_pack_device(self._vis.data_ptr(), self._agent.data_ptr(), self.x_dim, self.y_dim)
         return self._obs_dict()
 
+    def _stage_host_actions(self, actions):
+        """numpy integer actions -> the device through pinned int64 staging buffers (two, used
+        alternately) and an asynchronous copy on the step's stream (torch.as_tensor of a
+        pageable array is a synchronous copy; tools/prof_vec_step.py).  A buffer's event keeps
+        a later call from overwriting it before its copy has read it."""
+        n = self.num_envs
+        if getattr(self, "_pin", None) is None:
+            self._pin = [torch.empty(n, dtype=torch.int64, pin_memory=True) for _ in range(2)]
+            self._pin_done = [torch.cuda.Event(), torch.cuda.Event()]
+            for ev in self._pin_done:
+                ev.record()
+            self._act64 = torch.empty(n, dtype=torch.int64, device=self.device)
+            self._pin_k = 0
+        k = self._pin_k = self._pin_k ^ 1
+        self._pin_done[k].synchronize()
+        np.copyto(self._pin[k].numpy(), actions, casting="unsafe")   # integer widening only
+        self._act64.copy_(self._pin[k], non_blocking=True)
+        self._pin_done[k].record()
+        return self._act64
+
     def _step_obs_dict(self):
         """_obs_dict after step_gym_device, which wrote the agent's (x, y) into _loc itself."""
         if self.observation == "compact":
@@ -196,7 +216,10 @@ class SPaRCVecEnv:
         overwritten by the next step (the reference returns its planes by reference too)."""
         self._stream()
         n = self.num_envs
-        a = torch.as_tensor(actions, device=self.device)
+        if isinstance(actions, np.ndarray) and actions.shape == (n,) and actions.dtype.kind in "iu":
+            a = self._stage_host_actions(actions)
+        else:
+            a = torch.as_tensor(actions, device=self.device)
         if a.shape != (n,):
             raise ValueError(f"actions must have shape ({n},)")
         if a.dtype not in (torch.uint8, torch.int32, torch.int64):
