@@ -37,6 +37,11 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "sparc-gym_amd"))
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles per SIMD
+# (MI355X_MICROARCH.md, Wave scheduling), at the 2.4 GHz peak engine clock
+VALU_PEAK_WAVE_INSTS = 1024 * 2.4e9 / 2
+CSRC_FILES = ("sparc-gym_amd/csrc/sparc_kernels.hip", "sparc-gym_amd/csrc/sparc_env.hpp",
+              "sparc-gym_amd/csrc/sparc_rules.hpp", "include/sparc_gym_amd.h", "sparc-gym_amd/Makefile")
 
 CONFIGS = {
     # name: (grid sizes, full property set, traceback, 'new' observation planes every step)
@@ -59,6 +64,8 @@ def parse():
                     help="env-steps per env in one bench step = one rollout launch (0 = 2,000; with "
                          "observation traces (c4) 50)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
+    ap.add_argument("--rehearsal", action="store_true",
+                    help="allow more ranks than GPUs (ranks share GPUs: a rehearsal, never a measurement)")
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--mode", default="rollout", choices=["rollout", "step"])
     ap.add_argument("--puzzles", type=int, default=1024)
@@ -122,26 +129,80 @@ def cpu_baseline(proc, tb, max_steps, seconds, obs_dims=None, config="c3"):
     try:
         r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=seconds * 4 + 120)
         mc = json.loads(r.stdout.strip().splitlines()[-1])
+        phys, logical, aff, quota = physical_cores()
         out.update(value=mc["value"], cores=mc["procs"],
                    sample=out["sample"] +
-                   f"; all-cores value: {mc['procs']} processes x {n} envs (oracle/cpu_bench.py), "
-                   f"{mc['seconds']:.0f} s, {mc['usable_cores']} usable cores")
+                   f"; value: {mc['procs']} processes x {n} envs (oracle/cpu_bench.py), "
+                   f"{mc['seconds']:.0f} s, one per core of this GPU's share of the host",
+                   per_core=round(mc["value"] / mc["procs"], 1),
+                   host={"physical_cores": phys, "logical_cpus": logical, "affinity_cpus": aff,
+                         "cgroup_cpu_quota": quota,
+                         "note": "the GPU box gives one GPU's job a 16-core share (its process rules); "
+                                 "whole_host_estimate = per_core x physical_cores is a linear estimate, "
+                                 "not a measurement"})
+        if phys:
+            out["whole_host_estimate"] = round(mc["value"] / mc["procs"] * phys, 1)
     except (subprocess.SubprocessError, ValueError, KeyError, IndexError) as exc:   # keep the 1-core number
         out["multi_core_error"] = repr(exc)[:200]
     return out
 
 
+def csrc_hash():
+    """sha256 (16 hex) of the kernel sources + ABI header + Makefile: the build a committed
+    counter summary belongs to."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in CSRC_FILES:
+        h.update(f.encode())
+        h.update(open(os.path.join(REPO, f), "rb").read())
+    return h.hexdigest()[:16]
+
+
 def load_traffic(workload, kernel):
-    """HBM bytes per launch from a committed rocprofv3 --pmc summary (profiles/pmc_traffic.json),
-    produced by tools/pmc_traffic.py; None when absent."""
+    """The committed rocprofv3 --pmc summary of this workload's kernel (profiles/pmc_traffic.json,
+    written by tools/pmc_traffic.py): {"bytes": HBM bytes per launch, "counters": SQ counters
+    per launch, "csrc_hash": ...}, or None when absent or recorded for other kernel sources
+    (then bench reports traffic: null rather than another build's counters)."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None
     try:
-        d = json.load(open(path))
-        return d.get(workload, {}).get(kernel)
+        e = json.load(open(path)).get(workload, {}).get(kernel)
     except (OSError, ValueError):
         return None
+    if not isinstance(e, dict) or e.get("csrc_hash") != csrc_hash():
+        return None
+    return e
+
+
+def physical_cores():
+    """(physical cores, logical CPUs) of the host from /proc/cpuinfo, and the CPUs this process
+    may use: its affinity set and its cgroup CPU quota (cpu.max), as (affinity, quota)."""
+    phys, logical = set(), 0
+    try:
+        cur = {}
+        for line in open("/proc/cpuinfo"):
+            if not line.strip():
+                if cur:
+                    logical += 1
+                    phys.add((cur.get("physical id"), cur.get("core id")))
+                cur = {}
+                continue
+            k, _, v = line.partition(":")
+            cur[k.strip()] = v.strip()
+        if cur:
+            logical += 1
+            phys.add((cur.get("physical id"), cur.get("core id")))
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return len(phys) or None, logical or os.cpu_count(), aff, quota
 
 
 def main():
@@ -152,8 +213,13 @@ def main():
     from sparc_gym_amd import dist as sdist
     from sparc_gym_amd.puzzles import pack_table, process_puzzles
 
-    rank, world, local = sdist.init_from_env(args.backend)
-    local = local % max(1, torch.cuda.device_count())   # (rehearsals: several ranks on one GPU)
+    ndev = torch.cuda.device_count()
+    local_env = int(os.environ.get("LOCAL_RANK", "0"))
+    if local_env >= ndev and not args.rehearsal:
+        raise SystemExit(f"LOCAL_RANK {local_env} but only {ndev} GPU(s) visible: one rank per GPU "
+                         f"(--rehearsal lets ranks share GPUs, for tests only)")
+    rank, world, local = sdist.init_from_env(args.backend, device=local_env % max(1, ndev))
+    local = local_env % max(1, ndev)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -254,12 +320,29 @@ def main():
     else:
         kernel = "k_rollout"
     workload = f"{args.config}_{args.mode}_n{n}_chunk{chunk if args.mode == 'rollout' else 1}"
-    traffic = load_traffic(workload, kernel)
+    pmc = load_traffic(workload, kernel)
+    traffic = pmc["bytes"] if pmc else None
+    issue = None
+    if pmc and "SQ_INSTS_VALU" in pmc.get("counters", {}):
+        valu = pmc["counters"]["SQ_INSTS_VALU"]
+        wave_steps = n / 64.0 * avg_T
+        issue = {"valu_wave_insts_per_launch": int(valu),
+                 "valu_per_wave_step": round(valu / wave_steps, 2),
+                 "salu_per_wave_step": round(pmc["counters"].get("SQ_INSTS_SALU", 0) / wave_steps, 2),
+                 "lds_per_wave_step": round(pmc["counters"].get("SQ_INSTS_LDS", 0) / wave_steps, 2),
+                 "peak_wave_insts_per_s": VALU_PEAK_WAVE_INSTS,
+                 "frac": round(valu / (avg_ms * 1e-3) / VALU_PEAK_WAVE_INSTS, 4),
+                 "note": "VALU issue roofline: SQ_INSTS_VALU of the committed PMC pass / the live kernel time / "
+                         "(1,024 SIMDs x one wave64 VALU per 2 cycles x 2.4 GHz)"}
+    backend = dist.get_backend() if dist.is_initialized() else None
+    observed_world = dist.get_world_size() if dist.is_initialized() else 1
     out = {
         "metric": "env-steps/sec at 65,536 envs, 7x7 grid (HBM roofline fraction in 'roofline')",
         "value": round(value, 1),
         "unit": "env-steps/s",
         "n_gpus": world,
+        "world_observed": {"world_size": observed_world, "backend": backend, "gpus_visible": ndev,
+                           "rehearsal": bool(args.rehearsal)},
         "steps": K,
         "warmup": W,
         "ms_per_step": round(elapsed * 1e3 / K, 6),   # per bench step: T env-steps of every env
@@ -275,10 +358,14 @@ def main():
                                   f"[N, {X}, {Y}] written every step" if obs else ""),
                    "mode": args.mode, "envs_per_gpu": n, "env_steps_per_bench_step": T,
                    "env_steps_per_launch": T,
-                   "parallelism": f"dp{world} (env shards, {'RCCL' if args.backend == 'nccl' else args.backend} "
+                   "parallelism": f"dp{world} (env shards, "
+                                  f"{'RCCL' if backend == 'nccl' else (backend or 'no')} "
                                   f"all_gather of per-env stats at end of batch)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
+                     "traffic_source": (f"profiles/pmc_traffic.json [{workload}][{kernel}], csrc {csrc_hash()}"
+                                        if pmc else f"none recorded for csrc {csrc_hash()}"),
+                     "issue": issue,
                      "kernel": kernel, "kernel_avg_ms": round(avg_ms, 4), "launches": len(kern_ms),
                      "algorithmic_bytes_per_launch": int(bytes_launch),
                      "bytes_model": f"per env-step {per_step} B (action, reward code, flags"

@@ -925,6 +925,22 @@ int fail(Ctx* c, int code, const std::string& m) {
             return fail((c), SPARC_E_HIP, std::string(#expr ": ") + hipGetErrorString(_e)); \
     } while (0)
 
+// Every ABI entry point leaves the caller's current device as it found it: check_ctx (and
+// create / destroy / sync) switch to the context's device for the call, and this guard, declared
+// first in the entry point, switches back on return.
+struct DevGuard {
+    int dev = -1;
+    DevGuard() {
+        if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+    }
+    ~DevGuard() {
+        int cur = -1;
+        if (dev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != dev) (void)hipSetDevice(dev);
+    }
+    DevGuard(const DevGuard&) = delete;
+    DevGuard& operator=(const DevGuard&) = delete;
+};
+
 Params make_params(const Ctx* c) {
     Params p{};
     p.tab.open = c->t_open;
@@ -954,16 +970,17 @@ Params make_params(const Ctx* c) {
 
 inline dim3 grid_for(size_t n) { return dim3((unsigned)((n + kBlock - 1) / kBlock)); }
 
-// lift a kernel's dynamic-LDS limit to kMaxDynLds once per process (the call is not free, and
-// a rollout call should cost one launch: it sits inside the bench's timed region)
-void allow_big_lds(const void* kern) {
+// lift a kernel's dynamic-LDS limit to kMaxDynLds once per (device, kernel) (the call is not
+// free, and a rollout call should cost one launch: it sits inside the bench's timed region)
+int allow_big_lds(Ctx* c, const void* kern) {
     static std::mutex mu;
-    static std::vector<const void*> done;
+    static std::vector<std::pair<int, const void*>> done;
     std::lock_guard<std::mutex> lock(mu);
-    for (const void* k : done)
-        if (k == kern) return;
-    (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxDynLds);
-    done.push_back(kern);
+    for (const auto& k : done)
+        if (k.first == c->device && k.second == kern) return SPARC_OK;
+    HIPCHK(c, hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxDynLds));
+    done.emplace_back(c->device, kern);
+    return SPARC_OK;
 }
 
 // call f(integral_constant<W>, bool_constant<TB>) for the runtime (W, TB)
@@ -1001,6 +1018,7 @@ const char* sparc_last_error(const void* ctx) {
 }
 
 int sparc_create(int device, const sparc_config* cfg, void** ctx_out) {
+    DevGuard dg;
     if (!cfg || !ctx_out) return fail(nullptr, SPARC_E_INVALID, "null argument");
     *ctx_out = nullptr;
     if (cfg->num_envs < 1) return fail(nullptr, SPARC_E_INVALID, "num_envs must be >= 1");
@@ -1046,6 +1064,7 @@ int sparc_create(int device, const sparc_config* cfg, void** ctx_out) {
 }
 
 int sparc_destroy(void* ctx) {
+    DevGuard dg;
     Ctx* c = static_cast<Ctx*>(ctx);
     if (!c) return SPARC_OK;
     (void)hipSetDevice(c->device);
@@ -1061,6 +1080,7 @@ int sparc_destroy(void* ctx) {
 }
 
 int sparc_set_stream(void* ctx, void* stream) {
+    DevGuard dg;
     Ctx* c = static_cast<Ctx*>(ctx);
     if (!c) return fail(nullptr, SPARC_E_INVALID, "null context");
     c->stream = static_cast<hipStream_t>(stream);   // NULL is the HIP null stream, used as such
@@ -1068,6 +1088,7 @@ int sparc_set_stream(void* ctx, void* stream) {
 }
 
 int sparc_use_own_stream(void* ctx) {
+    DevGuard dg;
     Ctx* c = static_cast<Ctx*>(ctx);
     if (!c) return fail(nullptr, SPARC_E_INVALID, "null context");
     c->stream = c->own;
@@ -1075,6 +1096,7 @@ int sparc_use_own_stream(void* ctx) {
 }
 
 int sparc_sync(void* ctx) {
+    DevGuard dg;
     Ctx* c = static_cast<Ctx*>(ctx);
     if (!c) return fail(nullptr, SPARC_E_INVALID, "null context");
     HIPCHK(c, hipSetDevice(c->device));
@@ -1092,6 +1114,7 @@ int sparc_sync(void* ctx) {
 }
 
 int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
+    DevGuard dg;
     Ctx* c = static_cast<Ctx*>(ctx);
     if (!c || !t || !t->open || !t->info) return fail(c, SPARC_E_INVALID, "null argument");
     if (t->num_puzzles < 1) return fail(c, SPARC_E_INVALID, "empty puzzle table");
@@ -1228,6 +1251,7 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
 }
 
 int sparc_reset_device(void* ctx, const uint32_t* d_q, const uint8_t* d_mask, uint8_t* d_flags) {
+    DevGuard dg;
     Ctx* c = static_cast<Ctx*>(ctx);
     int rc = check_ctx(c, false);
     if (rc) return rc;
@@ -1244,6 +1268,7 @@ int sparc_reset_device(void* ctx, const uint32_t* d_q, const uint8_t* d_mask, ui
 }
 
 int sparc_reset_host(void* ctx, const uint32_t* q, const uint8_t* mask, uint8_t* flags) {
+    DevGuard dg;
     Ctx* c = static_cast<Ctx*>(ctx);
     int rc = check_ctx(c, false);
     if (rc) return rc;
@@ -1259,6 +1284,7 @@ int sparc_reset_host(void* ctx, const uint32_t* q, const uint8_t* mask, uint8_t*
 }
 
 int sparc_step_device(void* ctx, const uint8_t* d_act, int8_t* d_rew, uint8_t* d_flags) {
+    DevGuard dg;
     Ctx* c = static_cast<Ctx*>(ctx);
     int rc = check_ctx(c, true);
     if (rc) return rc;
@@ -1272,6 +1298,7 @@ int sparc_step_device(void* ctx, const uint8_t* d_act, int8_t* d_rew, uint8_t* d
 }
 
 int sparc_step_host(void* ctx, const uint8_t* act, int8_t* rew, uint8_t* flags) {
+    DevGuard dg;
     Ctx* c = static_cast<Ctx*>(ctx);
     int rc = check_ctx(c, true);
     if (rc) return rc;
@@ -1297,6 +1324,7 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
     if ((uint64_t)T * c->n > (1ull << 40)) return fail(c, SPARC_E_INVALID, "T*N too large");
     const Params p = make_params(c);
     const ObsTrace no_obs{nullptr, nullptr, 1u, 1u};
+    int lds_rc = SPARC_OK;   // allow_big_lds failure inside a launch lambda (then no launch)
     int4* st = reinterpret_cast<int4*>(d_stats);
     auto aligned = [](const void* q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & 15u) == 0; };
     const uint32_t tiled = (c->n % 16 == 0) && aligned(d_act) && aligned(d_rew) && aligned(d_flags);
@@ -1319,7 +1347,7 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
             const bool lds_s = kS_Base + tbytes <= budget;
             const size_t shm_s = kS_Base + (lds_s ? tbytes : 0);
             auto launch_s = [&](auto kern, const uint8_t* a) {
-                if (shm_s > 64 * 1024) allow_big_lds(reinterpret_cast<const void*>(kern));
+                if (shm_s > 64 * 1024 && (lds_rc = allow_big_lds(c, reinterpret_cast<const void*>(kern)))) return;
                 kern<<<dim3((unsigned)blocks), kBlock1s, shm_s, c->stream>>>(p, T16, a, seed, t0, d_rew, d_flags, st);
             };
             auto go_s = [&](auto tb) {
@@ -1334,6 +1362,7 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
             };
             if (c->cfg.traceback) go_s(std::true_type{});
             else go_s(std::false_type{});
+            if (lds_rc) return lds_rc;
             rc = launch_check(c);
             if (rc || T16 == T) return rc;
             const size_t adv = (size_t)T16 * c->n;
@@ -1347,7 +1376,7 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
         const bool lds_table = kW1Base + tbytes <= budget;
         const size_t shm = kW1Base + (lds_table ? tbytes : 0);
         auto launch = [&](auto kern, const uint8_t* a) {
-            if (shm > 64 * 1024) allow_big_lds(reinterpret_cast<const void*>(kern));
+            if (shm > 64 * 1024 && (lds_rc = allow_big_lds(c, reinterpret_cast<const void*>(kern)))) return;
             kern<<<dim3((unsigned)blocks), kBlock1, shm, c->stream>>>(p, T, a, seed, t0, d_rew, d_flags, st, tiled);
         };
         auto go1 = [&](auto tb) {
@@ -1362,6 +1391,7 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
         };
         if (c->cfg.traceback) go1(std::true_type{});
         else go1(std::false_type{});
+        if (lds_rc) return lds_rc;
         return launch_check(c);
     }
     dispatch_w_tb(c->W, c->cfg.traceback, [&](auto w, auto tb) {
@@ -1380,7 +1410,7 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
             const size_t shm = base + (lds_table ? tbytes : 0);
             const dim3 g((unsigned)blocks);
             auto launch = [&](auto kern, const uint8_t* a) {
-                if (shm > 64 * 1024) allow_big_lds(reinterpret_cast<const void*>(kern));
+                if (shm > 64 * 1024 && (lds_rc = allow_big_lds(c, reinterpret_cast<const void*>(kern)))) return;
                 kern<<<g, kBlock, shm, c->stream>>>(p, T, a, seed, t0, d_rew, d_flags, st, tiled, ot ? *ot : no_obs);
             };
             if (d_act) {
@@ -1395,6 +1425,7 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
         else if (half) go(std::integral_constant<int, 32>{}, std::false_type{});
         else go(std::integral_constant<int, 64>{}, std::false_type{});
     });
+    if (lds_rc) return lds_rc;
     return launch_check(c);
 }
 
@@ -1415,6 +1446,7 @@ int sparc_rollout_device(void* ctx, int32_t T, const uint8_t* d_act, uint64_t se
 int sparc_rollout_obs_device(void* ctx, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_t t0,
                              int8_t* d_rew, uint8_t* d_flags, int32_t* d_stats, int32_t* d_visited,
                              int32_t* d_agent, int32_t x_dim, int32_t y_dim) {
+    DevGuard dg;
     Ctx* c = static_cast<Ctx*>(ctx);
     if (!c) return fail(nullptr, SPARC_E_INVALID, "null context");
     int rc = check_obs_dims(c, x_dim, y_dim);
@@ -1426,6 +1458,7 @@ int sparc_rollout_obs_device(void* ctx, int32_t T, const uint8_t* d_act, uint64_
 
 int sparc_step_obs_device(void* ctx, const uint8_t* d_act, int8_t* d_rew, uint8_t* d_flags, int32_t* d_visited,
                           int32_t* d_agent, int32_t x_dim, int32_t y_dim, uint32_t* d_puzzle, uint32_t* d_xy) {
+    DevGuard dg;
     Ctx* c = static_cast<Ctx*>(ctx);
     int rc = check_ctx(c, true);
     if (rc) return rc;
@@ -1445,6 +1478,7 @@ int sparc_step_gym_device(void* ctx, const void* d_act, int32_t action_bytes, do
                           uint8_t* d_trunc, uint8_t* d_legal, uint8_t* d_areset, int8_t* d_rew_code,
                           uint8_t* d_flags, int32_t* d_visited, int32_t* d_agent, int32_t x_dim, int32_t y_dim,
                           uint32_t* d_puzzle, int32_t* d_loc) {
+    DevGuard dg;
     Ctx* c = static_cast<Ctx*>(ctx);
     int rc = check_ctx(c, true);
     if (rc) return rc;
@@ -1467,6 +1501,7 @@ int sparc_step_gym_device(void* ctx, const void* d_act, int32_t action_bytes, do
 }
 
 int sparc_obs_pack_device(void* ctx, int32_t* d_vis, int32_t* d_agent, int32_t xd, int32_t yd) {
+    DevGuard dg;
     Ctx* c = static_cast<Ctx*>(ctx);
     int rc = check_ctx(c, true);
     if (rc) return rc;
@@ -1481,6 +1516,7 @@ int sparc_obs_pack_device(void* ctx, int32_t* d_vis, int32_t* d_agent, int32_t x
 }
 
 int sparc_load_rules(void* ctx, const sparc_rules_table* t) {
+    DevGuard dg;
     Ctx* c = static_cast<Ctx*>(ctx);
     int rc = check_ctx(c, false);
     if (rc) return rc;
@@ -1552,6 +1588,7 @@ int sparc_load_rules(void* ctx, const sparc_rules_table* t) {
 }
 
 int sparc_rules_device(void* ctx, uint16_t* d_bits, uint8_t* d_region, uint64_t* d_fit) {
+    DevGuard dg;
     Ctx* c = static_cast<Ctx*>(ctx);
     int rc = check_ctx(c, true);
     if (rc) return rc;
@@ -1567,6 +1604,7 @@ int sparc_rules_device(void* ctx, uint16_t* d_bits, uint8_t* d_region, uint64_t*
 }
 
 int sparc_rules_host(void* ctx, uint16_t* bits, uint8_t* region, uint64_t* fit) {
+    DevGuard dg;
     Ctx* c = static_cast<Ctx*>(ctx);
     int rc = check_ctx(c, true);
     if (rc) return rc;
@@ -1585,6 +1623,7 @@ int sparc_rules_host(void* ctx, uint16_t* bits, uint8_t* region, uint64_t* fit) 
 }
 
 int sparc_read_state(void* ctx, const sparc_state_host* o) {
+    DevGuard dg;
     Ctx* c = static_cast<Ctx*>(ctx);
     int rc = check_ctx(c, true);
     if (rc) return rc;
@@ -1610,6 +1649,7 @@ int sparc_read_state(void* ctx, const sparc_state_host* o) {
 }
 
 int sparc_state_ptr(void* ctx, int32_t which, void** d_ptr) {
+    DevGuard dg;
     Ctx* c = static_cast<Ctx*>(ctx);
     if (!c || !d_ptr) return fail(c, SPARC_E_INVALID, "null argument");
     switch (which) {
@@ -1625,6 +1665,7 @@ int sparc_state_ptr(void* ctx, int32_t which, void** d_ptr) {
 }
 
 int sparc_copy_state_device(void* ctx, int32_t which, void* d_out) {
+    DevGuard dg;
     Ctx* c = static_cast<Ctx*>(ctx);
     int rc = check_ctx(c, true);
     if (rc) return rc;

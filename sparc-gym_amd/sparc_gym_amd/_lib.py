@@ -9,7 +9,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("SPARC_DIAG_LIB") or os.path.join(_HERE, "libsparc_gym_amd.so")
+LIB_PATH = os.path.join(_HERE, "libsparc_gym_amd.so")   # the in-tree gfx950 build; no override
 
 SPARC_OK = 0
 AUTORESET = {"none": 0, "next_step": 1}
@@ -79,9 +79,14 @@ class SparcError(RuntimeError):
 
 
 def load(path=LIB_PATH):
-    """Load and type the HIP library (cached).  Raises if it is missing: no CPU fallback."""
+    """Load and type the HIP library (cached).  Raises if it is missing: no CPU fallback.
+
+    The product path always loads the in-tree build.  Profiling tools may load another build
+    of the same ABI by calling ``load(path)`` themselves before any env is created."""
     global _lib
     if _lib is not None:
+        if os.path.abspath(path) != _lib._sparc_path:
+            raise ImportError(f"libsparc_gym_amd already loaded from {_lib._sparc_path}")
         return _lib
     if not os.path.exists(path):
         raise ImportError(f"{path} not found: build the HIP extension (make -C sparc-gym_amd)")
@@ -92,6 +97,7 @@ def load(path=LIB_PATH):
         f.restype = res
     if lib.sparc_abi_version() != 1:
         raise ImportError("libsparc_gym_amd ABI version mismatch")
+    lib._sparc_path = os.path.abspath(path)
     _lib = lib
     return lib
 

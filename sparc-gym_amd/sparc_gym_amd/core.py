@@ -46,6 +46,7 @@ class SparcCore:
                                   trie.ctypes.data if len(trie) else None)
         self._check(self.lib.sparc_load_puzzles(self.ctx, ctypes.byref(t)))
         self.table = table
+        self.has_state = False   # as the context: the old state may name puzzles that are gone
 
     def load_rules(self, rt: RulesTable):
         """Upload the rule-audit table (puzzles.pack_rules) for the loaded puzzles."""
@@ -112,6 +113,7 @@ class SparcCore:
             raise ValueError("mask shape mismatch")
         flags = np.zeros(self.num_envs, np.uint8)
         self._check(self.lib.sparc_reset_host(self.ctx, _ptr(q), _ptr(m), _ptr(flags)))
+        self.has_state = True
         return flags
 
     def step_host(self, actions):
@@ -136,6 +138,7 @@ class SparcCore:
     # ---------------------------------------------------------------- device-pointer calls (async)
     def reset_device(self, d_puzzle_index, d_mask=None, d_flags=None):
         self._check(self.lib.sparc_reset_device(self.ctx, d_puzzle_index, d_mask, d_flags))
+        self.has_state = True
 
     def step_device(self, d_actions, d_reward, d_flags):
         self._check(self.lib.sparc_step_device(self.ctx, d_actions, d_reward, d_flags))

@@ -21,15 +21,17 @@ def env_shard(envs_per_rank: int, rank: int):
     return rank * envs_per_rank, envs_per_rank
 
 
-def init_from_env(backend="nccl"):
-    """Initialise torch.distributed from torchrun's environment; returns (rank, world, local)."""
+def init_from_env(backend="nccl", device=None):
+    """Initialise torch.distributed from torchrun's environment; returns (rank, world, local).
+    ``device``: this rank's GPU (default LOCAL_RANK, one process per GPU)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and not dist.is_initialized():
         if backend == "nccl":
-            torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dev = local if device is None else device
+            torch.cuda.set_device(dev)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group(backend)
     return rank, world, local

@@ -39,6 +39,28 @@ def reward_value(code):
     return _REWARD[int(code)]
 
 
+def text_grid_rows(raw):
+    """The 'SPaRC' text grid (rows of one-character strings, row = y) from a puzzle's
+    ``puzzle_array`` in any of the three forms _load_puzzle accepts (SPaRC_Gym.py:153-164):
+    a 1-D object array of row arrays (parquet), a 2-D array, or nested sequences.  Always a
+    fresh list of lists, which step() edits in place."""
+    if isinstance(raw, np.ndarray) and raw.dtype == object and raw.ndim == 1:
+        grid_rows = [r.astype(str).tolist() for r in raw]
+    elif isinstance(raw, np.ndarray) and raw.ndim == 2:
+        grid_rows = raw.astype(str).tolist()
+    else:
+        grid_rows = [[str(c) for c in row] for row in raw]
+    w = len(grid_rows[0])
+    if any(len(r) != w for r in grid_rows):
+        raise ValueError("Non-rectangular SPaRC grid")
+    return grid_rows
+
+
+def text_obs(grid_rows):
+    """_build_json_obs (SPaRC_Gym.py:988-992)."""
+    return json.dumps(grid_rows, separators=(",", ":"))
+
+
 def action_code(action):
     """Map a caller's action to 0..3, or 255 if `action in legal_actions` can never hold."""
     for k in range(4):
@@ -119,17 +141,7 @@ class SPaRC_Gym(Env):
         self.color_array = puzzle["color_array"]
         self.additional_info = puzzle["additional_info"]
         if self.observation == "SPaRC":                                              # 153-164
-            raw = puzzle["observ"]
-            if isinstance(raw, np.ndarray) and raw.dtype == object and raw.ndim == 1:
-                grid_rows = [r.astype(str).tolist() for r in raw]
-            elif isinstance(raw, np.ndarray) and raw.ndim == 2:
-                grid_rows = raw.astype(str).tolist()
-            else:
-                grid_rows = [[str(c) for c in row] for row in raw]
-            w = len(grid_rows[0])
-            if any(len(r) != w for r in grid_rows):
-                raise ValueError("Non-rectangular SPaRC grid")
-            self.observ = grid_rows
+            self.observ = text_grid_rows(puzzle["observ"])
         self.start_location = puzzle["start_location"]
         self.target_location = puzzle["target_location"]
         self.solution_paths = puzzle["solution_paths"]
@@ -230,7 +242,7 @@ class SPaRC_Gym(Env):
         raise ValueError("Invalid observation type. Choose 'new' or 'SPaRC'.")
 
     def _build_json_obs(self):
-        return json.dumps(self.observ, separators=(",", ":"))
+        return text_obs(self.observ)
 
     def _validate_rules(self, terminated=False, truncated=False):
         """_validate_rules (SPaRC_Gym.py:941-950): the audit runs in the k_rules kernel."""

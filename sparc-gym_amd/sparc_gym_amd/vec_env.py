@@ -44,11 +44,16 @@ REWARD_SCALE = 100.0
 class SPaRCVecEnv:
     def __init__(self, num_envs, puzzles=None, df_name="lkaesberg/SPaRC", df_split="all", df_set="test",
                  observation="new", traceback=False, max_steps=2000, autoreset="next_step", device=0,
-                 env_offset=0, pitch=None, words=None, processed=None, table=None, rules=False):
+                 env_offset=0, pitch=None, words=None, processed=None, table=None, rules=False, copy=True):
         if observation not in ("new", "compact"):
             raise ValueError("observation must be 'new' or 'compact' for the vector env")
         self.num_envs = int(num_envs)
         self.observation = observation
+        # copy=True (gymnasium's vector-env default): every step() returns observation tensors
+        # of its own, so an (obs, next_obs) pair kept by the caller stays intact; copy=False
+        # returns the env's buffers, overwritten in place by the next step (the reference's
+        # by-reference planes, SPaRC_Gym.py:979)
+        self.copy = bool(copy)
         self.traceback = bool(traceback)
         self.max_steps = max_steps
         self.autoreset = autoreset
@@ -116,39 +121,60 @@ class SPaRCVecEnv:
             self.core.obs_pack_device(self._vis.data_ptr(), self._agent.data_ptr(), self.x_dim, self.y_dim)
         return self._obs_dict()
 
-    def _stage_host_actions(self, actions):
+    def _stage_host_actions(self, actions, stream):
         """numpy integer actions -> the device through pinned int64 staging buffers (two, used
         alternately) and an asynchronous copy on the step's stream (torch.as_tensor of a
-        pageable array is a synchronous copy; tools/prof_vec_step.py).  A buffer's event keeps
-        a later call from overwriting it before its copy has read it."""
+        pageable array is a synchronous copy; tools/prof_vec_step.py).  A buffer's event,
+        recorded on the stream that runs its copy, keeps a later call from overwriting it before
+        the copy has read it.  The device copy is a fresh allocation on that stream (the caching
+        allocator orders its reuse on the stream), so a caller that switches streams between
+        steps cannot overwrite actions a previous step's kernel is still reading."""
         n = self.num_envs
         if getattr(self, "_pin", None) is None:
             self._pin = [torch.empty(n, dtype=torch.int64, pin_memory=True) for _ in range(2)]
-            self._pin_done = [torch.cuda.Event(), torch.cuda.Event()]
-            for ev in self._pin_done:
-                ev.record()
-            self._act64 = torch.empty(n, dtype=torch.int64, device=self.device)
+            self._pin_done = [None, None]
             self._pin_k = 0
         k = self._pin_k = self._pin_k ^ 1
-        self._pin_done[k].synchronize()
+        if self._pin_done[k] is not None:
+            self._pin_done[k].synchronize()
         np.copyto(self._pin[k].numpy(), actions, casting="unsafe")   # integer widening only
-        self._act64.copy_(self._pin[k], non_blocking=True)
-        self._pin_done[k].record()
-        return self._act64
+        act = torch.empty(n, dtype=torch.int64, device=self.device)
+        act.copy_(self._pin[k], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        self._pin_done[k] = ev
+        return act
 
-    def _step_obs_dict(self):
-        """_obs_dict after step_gym_device, which wrote the agent's (x, y) into _loc itself."""
+    def _step_obs_dict(self, bufs):
+        """_obs_dict after step_gym_device, which wrote the agent's (x, y) into loc itself."""
+        vis, agent, pidx, loc = bufs
         if self.observation == "compact":
-            return {"puzzle_index": self._pidx, "agent_location": self._loc}
-        return {"visited": self._vis, "agent_location": self._agent, "puzzle_index": self._pidx,
-                "agent_xy": self._loc}
+            return {"puzzle_index": pidx, "agent_location": loc}
+        return {"visited": vis, "agent_location": agent, "puzzle_index": pidx, "agent_xy": loc}
+
+    def _step_obs_buffers(self):
+        """(visited, agent_location, puzzle_index, agent_xy) targets of one step: fresh tensors
+        with copy=True, else the env's own buffers."""
+        if not self.copy:
+            new = self.observation == "new"
+            return (self._vis if new else None, self._agent if new else None, self._pidx, self._loc)
+        n, dev = self.num_envs, self.device
+        vis = agent = None
+        if self.observation == "new":
+            vis = torch.empty((n, self.x_dim, self.y_dim), dtype=torch.int32, device=dev)
+            agent = torch.empty_like(vis)
+        return (vis, agent, torch.empty(n, dtype=torch.int32, device=dev),
+                torch.empty((n, 2), dtype=torch.int32, device=dev))
 
     def _obs_dict(self):
         loc = torch.stack([self._pos & 0xFF, (self._pos >> 8) & 0xFF], dim=1)
+        pidx = self._pidx.clone() if self.copy else self._pidx
         if self.observation == "compact":
-            return {"puzzle_index": self._pidx, "agent_location": loc}
-        return {"visited": self._vis, "agent_location": self._agent, "puzzle_index": self._pidx,
-                "agent_xy": loc}
+            return {"puzzle_index": pidx, "agent_location": loc}
+        if self.copy:
+            return {"visited": self._vis.clone(), "agent_location": self._agent.clone(), "puzzle_index": pidx,
+                    "agent_xy": loc}
+        return {"visited": self._vis, "agent_location": self._agent, "puzzle_index": pidx, "agent_xy": loc}
 
     def _load_rules(self):
         if self._rbits is None:
@@ -179,24 +205,45 @@ class SPaRCVecEnv:
         return self._np_random
 
     # ------------------------------------------------------------------ API
+    def current_puzzle_indices(self):
+        """[N] int64: each env's current puzzle index (the reference's current_puzzle_index),
+        read from the device, so it follows the device's autoresets.  Before the first
+        reset: env i -> i mod P (the vector form of __init__ loading puzzle 0, SPaRC_Gym.py:90)."""
+        if not self.core.has_state:
+            return self._cursor.copy()
+        cur = torch.empty(self.num_envs, dtype=torch.int32, device=self.device)
+        self.core.copy_state_device(4, cur.data_ptr())
+        return cur.cpu().numpy().astype(np.int64)
+
     def reset(self, seed=None, options=None):
         """Per-env puzzle choice as SPaRC_Gym.reset (SPaRC_Gym.py:1075-1087), vectorised:
-        options['puzzle_index'] ([N] ints) or options['puzzle_id'] ([N] ids) > seed
-        (Generator(PCG64(SeedSequence(seed))).integers(P, size=N)) > sequential (+1 mod P)."""
+        * options given: options['puzzle_index'] ([N] ints, this build's extension) or
+          options['puzzle_id'] (one id or [N] ids); an env whose id is missing (or any options
+          without either key, e.g. {}) keeps its current puzzle (1076-1082);
+        * else seed: Generator(PCG64(SeedSequence(seed))).integers(P, size=N) (1084-1085; env
+          0 gets the reference's index);
+        * else sequential: current index + 1 mod P (1087).
+        "Current" is the device's puzzle index, which next-step autoresets advance."""
         self._stream()
         P = self.num_puzzles
         if options is not None and "puzzle_index" in options:
             q = np.asarray(options["puzzle_index"], np.int64)
-        elif options is not None and "puzzle_id" in options:
-            ids = {p["id"]: i for i, p in reversed(list(enumerate(self.puzzles)))}
-            want = options["puzzle_id"]
-            want = [want] * self.num_envs if isinstance(want, str) else list(want)
-            q = np.array([ids.get(w, c) for w, c in zip(want, self._cursor)], np.int64)
+        elif options is not None:
+            cur = self.current_puzzle_indices()
+            want = options.get("puzzle_id", None)
+            if want is None:
+                q = cur
+            else:
+                ids = {p["id"]: i for i, p in reversed(list(enumerate(self.puzzles)))}
+                want = [want] * self.num_envs if isinstance(want, str) or not hasattr(want, "__len__") else list(want)
+                if len(want) != self.num_envs:
+                    raise ValueError(f"options['puzzle_id'] must be one id or {self.num_envs} ids")
+                q = np.array([ids.get(w, c) for w, c in zip(want, cur)], np.int64)
         elif seed is not None:
             self._np_random = np.random.Generator(np.random.PCG64(np.random.SeedSequence(seed)))
             q = self._np_random.integers(P, size=self.num_envs)
         else:
-            q = (self._cursor + 1) % P
+            q = (self.current_puzzle_indices() + 1) % P
         if q.shape != (self.num_envs,) or q.min() < 0 or q.max() >= P:
             raise ValueError("puzzle indices must be [num_envs] in [0, num_puzzles)")
         self._cursor = q.copy()
@@ -211,13 +258,13 @@ class SPaRCVecEnv:
         types: < 0 or >= 4 is illegal).  ONE launch (sparc_step_gym_device) writes the step, the
         post-step observation and the gym outputs: reward [N] float64 (the reference's exact
         values), terminated / truncated [N] bool, and info's legal_mask, autoreset and
-        reward_code.  reward / terminated / truncated / legal_mask / autoreset are fresh
-        tensors per call; the observation tensors and reward_code are the env's buffers,
-        overwritten by the next step (the reference returns its planes by reference too)."""
+        reward_code.  Every returned tensor is fresh per call (copy=True, the default); with
+        copy=False the observation tensors and reward_code are the env's buffers, overwritten
+        by the next step (the reference returns its planes by reference, SPaRC_Gym.py:979)."""
         self._stream()
         n = self.num_envs
         if isinstance(actions, np.ndarray) and actions.shape == (n,) and actions.dtype.kind in "iu":
-            a = self._stage_host_actions(actions)
+            a = self._stage_host_actions(actions, torch.cuda.current_stream(self.device))
         else:
             a = torch.as_tensor(actions, device=self.device)
         if a.shape != (n,):
@@ -235,15 +282,21 @@ class SPaRCVecEnv:
         legal = buf[10 * n:11 * n]
         autoreset = buf[11 * n:].view(torch.bool)
         new = self.observation == "new"
+        bufs = self._step_obs_buffers()
+        vis, agent, pidx, loc = bufs
         self.core.step_gym_device(a.data_ptr(), a.element_size(), reward.data_ptr(), terminated.data_ptr(),
                                   truncated.data_ptr(), legal.data_ptr(), autoreset.data_ptr(), self._rew.data_ptr(),
-                                  self._flags.data_ptr(), self._vis.data_ptr() if new else None,
-                                  self._agent.data_ptr() if new else None, self.x_dim if new else 1,
-                                  self.y_dim if new else 1, self._pidx.data_ptr(), self._loc.data_ptr())
-        info = {"legal_mask": legal, "autoreset": autoreset, "reward_code": self._rew}
+                                  self._flags.data_ptr(), vis.data_ptr() if new else None,
+                                  agent.data_ptr() if new else None, self.x_dim if new else 1,
+                                  self.y_dim if new else 1, pidx.data_ptr(), loc.data_ptr())
+        if self.copy:
+            self._loc = loc   # the latest agent (x, y), as the step path wrote it
+        info = {"legal_mask": legal, "autoreset": autoreset,
+                "reward_code": self._rew.clone() if self.copy else self._rew}
         if self.rules:
-            info["rule_bits"] = self.rule_audit()["bits"]
-        return self._step_obs_dict(), reward, terminated, truncated, info
+            bits = self.rule_audit()["bits"]
+            info["rule_bits"] = bits.clone() if self.copy else bits
+        return self._step_obs_dict(bufs), reward, terminated, truncated, info
 
     def rollout(self, T, actions=None, seed=0, t0=0, stats=None, record=True, out=None, obs=False, obs_out=None):
         """T steps of every env in ONE kernel launch.  actions: [T, N] uint8 on the GPU or None

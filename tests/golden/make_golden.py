@@ -32,6 +32,8 @@ REPO = os.path.dirname(os.path.dirname(HERE))
 REF = "/root/reference"
 sys.path.insert(0, os.path.join(REPO, "sparc-gym_amd"))
 from sparc_gym_amd import synthetic  # noqa: E402
+sys.path.insert(0, os.path.dirname(HERE))
+from golden_io import rows_as_ndarray  # noqa: E402
 
 
 def import_reference():
@@ -150,6 +152,62 @@ def run_episode(env, pristine, idx, strategy, rng, max_len=400, post_done=3):
     return rec
 
 
+def run_text_episode(env, pristine, idx, strategy, rng, max_len=120, post_done=2):
+    """One observation='SPaRC' episode: the JSON text grid after reset and every step
+    (SPaRC_Gym.py:153-164, 988-992, 1150-1184)."""
+    env.puzzles = copy.deepcopy(pristine)
+    pid = env.puzzles[idx]["id"]
+    obs, info = env.reset(options={"puzzle_id": pid})
+    rec = {"puzzle_index": idx, "puzzle_id": str(pid), "strategy": strategy, "reset_obs": obs,
+           "reset_legal": [int(a) for a in info["legal_actions"]], "actions": [], "steps": []}
+    sols = env.solution_paths[:env.solution_count]
+    plan = sol_actions(sols[int(rng.integers(len(sols)))]) if strategy == "solution" and sols else []
+    if strategy == "detour" and sols:
+        plan = sol_actions(sols[0])
+        if len(plan) > 2:
+            k = int(rng.integers(1, len(plan) - 1))
+            d = int(rng.integers(4))
+            plan = plan[:k] + [d, (d + 2) % 4, d, (d + 2) % 4] + plan[k:]
+    done_at, t = None, 0
+    while t < max_len:
+        if plan:
+            a = plan.pop(0)
+        elif strategy == "legal":
+            la = info["legal_actions"]
+            a = int(la[int(rng.integers(len(la)))]) if la else 0
+        else:
+            a = int(rng.choice([0, 1, 2, 3, 0, 1, 2, 3, 5]))
+        obs, r, term, trunc, info = env.step(a)
+        rec["actions"].append(a)
+        rec["steps"].append({"obs": obs, "reward": reward_repr(r), "terminated": bool(term),
+                             "truncated": bool(trunc), "legal_actions": [int(x) for x in info["legal_actions"]],
+                             "agent_location": [int(v) for v in info["agent_location"]]})
+        t += 1
+        if (term or trunc) and done_at is None:
+            done_at = t
+        if done_at is not None and t >= done_at + post_done:
+            break
+    return rec
+
+
+def text_episodes(records, tb, max_steps, n_eps, seed, tag, ndarray_rows=False):
+    """observation='SPaRC' episodes.  ndarray_rows: puzzle_array as a 1-D object array of
+    per-row string arrays, the form a parquet export of the dataset hands to the reference
+    (its first branch at SPaRC_Gym.py:155-156); otherwise lists of rows (the third branch)."""
+    df = synthetic.records_to_dataframe(records)
+    if ndarray_rows:
+        df["puzzle_array"] = [rows_as_ndarray(g) for g in df["puzzle_array"]]
+    REFMOD.load_dataset = lambda *a, **k: SimpleNamespace(to_pandas=lambda: df)
+    env = REFMOD.SPaRC_Gym(observation="SPaRC", traceback=tb, max_steps=max_steps)
+    pristine = copy.deepcopy(env.puzzles)
+    rng = np.random.default_rng(seed)
+    strategies = ["solution", "legal", "random", "detour"]
+    eps = [run_text_episode(env, pristine, int(rng.integers(len(pristine))), strategies[e % 4], rng)
+           for e in range(n_eps)]
+    return {"tag": tag, "traceback": tb, "max_steps": max_steps, "records": records,
+            "ndarray_rows": ndarray_rows, "episodes": eps}
+
+
 def episodes(records, tb, max_steps, strategies, n_eps, seed, tag):
     env = make_env(records, traceback=tb, max_steps=max_steps)
     pristine = copy.deepcopy(env.puzzles)
@@ -233,6 +291,10 @@ def main():
     out["poolD_tb1"] = episodes(poolD, True, 2000, rs, 24, 16, "edge puzzles (0 solutions, 3x3, 15x15, ...)")
     out["poolD_tb0"] = episodes(poolD, False, 2000, rs, 12, 17, "edge puzzles, traceback off")
     out["poolE_tb1"] = episodes(poolE, True, 2000, rs, 12, 18, "stale-symbol crafted cells")
+    # observation='SPaRC' (the text grid), both puzzle_array forms, traceback on / off
+    out["text_tb1"] = text_episodes(poolC, True, 300, 24, 19, "SPaRC text obs, mixed lattices, traceback")
+    out["text_tb0_nd"] = text_episodes(poolA, False, 40, 16, 20, "SPaRC text obs, 7x7, ndarray rows, max_steps=40",
+                                       ndarray_rows=True)
 
     # seeded / sequential / option resets (SPaRC_Gym.py:1075-1087)
     env = make_env(poolA, traceback=False, max_steps=2000)

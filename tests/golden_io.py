@@ -30,3 +30,23 @@ def oracle_puzzles(golden):
                     "target": p["target"], "solution_count": p["solution_count"],
                     "solution_paths": p["solution_paths"], "gaps": dense(p["base"]["gaps"])})
     return out
+
+
+def rows_as_ndarray(grid):
+    """list of rows -> 1-D object ndarray of per-row string ndarrays: the form a parquet export
+    of the dataset gives puzzle_array (make_golden.text_episodes(ndarray_rows=True))."""
+    out = np.empty(len(grid), dtype=object)
+    for k, r in enumerate(grid):
+        out[k] = np.array(r, dtype=object)
+    return out
+
+
+def text_dataframe(golden):
+    """The DataFrame a text-obs fixture was generated from (puzzle_array in its recorded form)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(GOLDEN), os.pardir, "sparc-gym_amd"))
+    from sparc_gym_amd import synthetic
+    df = synthetic.records_to_dataframe(golden["records"])
+    if golden.get("ndarray_rows"):
+        df["puzzle_array"] = [rows_as_ndarray(g) for g in df["puzzle_array"]]
+    return df

@@ -1,0 +1,149 @@
+"""GPU parity at BASELINE.json's full sizes (configs c2, c3, c4).
+
+* c2: exactly 4,096 envs, 7x7 base planes, traceback off, 2,000 steps in one launch, bit-exact
+  against the C oracle over every env (reward codes, flags, state, stats).
+* c3: 65,536 envs, 7x7 full property set, traceback on, max_steps = 37 so that truncation by
+  step count (SPaRC_Gym.py:1134) happens at full size, bit-exact against the oracle.
+* c4: 262,144 envs, mixed 5x5-11x11 lattices padded to 11x11, 'new' planes after every step
+  (the [T][N][11][11] int32 traces, 2 x 127 MB per step), autoresets inside the launch.  The
+  oracle replays ~2,000 sampled env columns (their puzzles and action columns; the envs are
+  independent) and every output of those columns must match; every env is checked with
+  size-independent invariants on the GPU: the agent plane is one-hot and inside the visited
+  plane, nothing lies outside the env's own lattice, the visited count moves by one per
+  moving step and restarts at 1 on a reset step, and at the end it equals path_len.
+"""
+import numpy as np
+import pytest
+
+from oracle import COracle
+from sparc_gym_amd import synthetic
+from sparc_gym_amd.puzzles import pack_table, process_puzzles
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def _oracle_pool(proc):
+    return [{"x_size": p["x_size"], "y_size": p["y_size"], "start": list(p["start_location"]),
+             "target": list(p["target_location"]), "solution_count": p["solution_count"],
+             "solution_paths": p["solution_paths"], "gaps": p["obs_array"]["gaps"]} for p in proc]
+
+
+def _bench_pool(sizes, full):
+    proc = process_puzzles(synthetic.make_puzzles(1024, seed=0, sizes=sizes, full_properties=full))
+    return proc, pack_table(proc)
+
+
+def _bench_pids(n):
+    return (np.arange(n, dtype=np.uint64) * 2654435761 % 1024).astype(np.int64)
+
+
+def _state_equal(s, so, table):
+    from sparc_gym_amd.core import visited_planes
+    for k, ko in (("x", "x"), ("y", "y"), ("step", "step"), ("path_len", "path_len"), ("puzzle", "pid"),
+                  ("outcome", "outcome")):
+        assert np.array_equal(s[k], so[ko]), k
+    assert np.array_equal(visited_planes(s["visited"], table, 16, 16), so["visited"].astype(np.int32))
+
+
+def test_c2_4096_envs_2000_steps_bit_exact(on_gpu):
+    from sparc_gym_amd import SPaRCVecEnv
+    proc, table = _bench_pool(((3, 3),), False)
+    n, T = 4096, 2000
+    pids = _bench_pids(n)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(42)
+    acts = torch.randint(0, 4, (T, n), dtype=torch.uint8, device="cuda", generator=g)
+    v = SPaRCVecEnv(n, processed=proc, table=table, traceback=False, observation="compact")
+    v.reset(options={"puzzle_index": pids})
+    st = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
+    out = v.rollout(T, acts, stats=st)
+    o = COracle(_oracle_pool(proc), n, False, 2000, autoreset=1)
+    o.reset(pids)
+    ost = np.zeros((n, 4), np.int32)
+    ro, fo = o.rollout(T, acts.cpu().numpy(), stats=ost)
+    assert np.array_equal(out["reward_code"].cpu().numpy(), ro)
+    assert np.array_equal(out["flags"].cpu().numpy(), fo)
+    assert np.array_equal(st.cpu().numpy(), ost)
+    _state_equal(v.state(), o.state(), table)
+    # and the in-kernel random actions at the same size
+    v.reset(options={"puzzle_index": pids})
+    out = v.rollout(T, None, seed=9)
+    o.reset(pids)
+    ro, fo = o.rollout(T, None, seed=9)
+    assert np.array_equal(out["reward_code"].cpu().numpy(), ro)
+    assert np.array_equal(out["flags"].cpu().numpy(), fo)
+
+
+def test_c3_65536_envs_step_count_truncation(on_gpu):
+    from sparc_gym_amd import SPaRCVecEnv
+    proc, table = _bench_pool(((3, 3),), True)
+    n, T, ms = 65536, 400, 37
+    pids = _bench_pids(n)
+    v = SPaRCVecEnv(n, processed=proc, table=table, traceback=True, max_steps=ms, observation="compact")
+    v.reset(options={"puzzle_index": pids})
+    st = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
+    out = v.rollout(T, None, seed=77, stats=st)
+    r, f = out["reward_code"].cpu().numpy(), out["flags"].cpu().numpy()
+    o = COracle(_oracle_pool(proc), n, True, ms, autoreset=1)
+    o.reset(pids)
+    ost = np.zeros((n, 4), np.int32)
+    ro, fo = o.rollout(T, None, seed=77, stats=ost)
+    assert np.array_equal(r, ro) and np.array_equal(f, fo)
+    assert np.array_equal(st.cpu().numpy(), ost)
+    _state_equal(v.state(), o.state(), table)
+    # truncation by step count did happen: a truncated step whose legal mask is not empty
+    trunc_steps = ((f & 2) != 0) & (((f >> 2) & 15) != 0)
+    assert trunc_steps.sum() > 1000
+
+
+def test_c4_262144_envs_new_planes_sampled_oracle_and_invariants(on_gpu):
+    from sparc_gym_amd import SPaRCVecEnv
+    proc, table = _bench_pool(((2, 2), (3, 3), (4, 4), (5, 5)), True)
+    n, T, ms = 262144, 12, 7                      # max_steps 7: autoresets inside the launch
+    pids = _bench_pids(n)
+    v = SPaRCVecEnv(n, processed=proc, table=table, traceback=True, max_steps=ms, observation="new")
+    v.reset(options={"puzzle_index": pids})
+    X, Y = v.x_dim, v.y_dim
+    assert (X, Y) == (11, 11) and table.words == 2
+    g = torch.Generator(device="cuda")
+    g.manual_seed(7)
+    acts = torch.randint(0, 4, (T, n), dtype=torch.uint8, device="cuda", generator=g)
+    out = v.rollout(T, acts, obs=True)
+    vis, ag = out["visited"], out["agent_location"]
+    f = out["flags"]
+    # --- sampled oracle columns (including the last envs: large-offset indexing)
+    rng = np.random.default_rng(0)
+    idx = np.unique(np.concatenate([rng.choice(n, 2000, replace=False), np.arange(n - 64, n), np.arange(64)]))
+    ti = torch.from_numpy(idx).cuda()
+    o = COracle(_oracle_pool(proc), len(idx), True, ms, autoreset=1)
+    o.reset(pids[idx])
+    ro, fo, vo, ao = o.rollout_obs(T, X, Y, np.ascontiguousarray(acts[:, ti].cpu().numpy()))
+    assert np.array_equal(out["reward_code"][:, ti].cpu().numpy(), ro)
+    assert np.array_equal(f[:, ti].cpu().numpy(), fo)
+    assert np.array_equal(vis[:, ti].cpu().numpy(), vo)
+    assert np.array_equal(ag[:, ti].cpu().numpy(), ao)
+    assert (fo & 64).any()
+    # --- every env: invariants on the GPU
+    xs = torch.tensor([p["x_size"] for p in proc], device="cuda")
+    ys = torch.tensor([p["y_size"] for p in proc], device="cuda")
+    resets = ((f & 64) != 0).to(torch.int64)
+    pid_t = (torch.from_numpy(pids).cuda()[None, :] + torch.cumsum(resets, 0)) % len(proc)   # [T, N]
+    cx = torch.arange(X, device="cuda").view(1, 1, X, 1)
+    cy = torch.arange(Y, device="cuda").view(1, 1, 1, Y)
+    outside = (cx >= xs[pid_t][..., None, None]) | (cy >= ys[pid_t][..., None, None])      # [T, N, X, Y]
+    assert not bool(((vis != 0) & outside).any())
+    assert not bool(((ag != 0) & outside).any())
+    assert bool((ag.sum((2, 3)) == 1).all())                       # one-hot agent plane
+    assert bool(((ag == 1) <= (vis == 1)).all())                   # the agent's point is visited
+    assert bool(((vis == 0) | (vis == 1)).all())
+    cnt = vis.sum((2, 3)).to(torch.int64)                          # [T, N] path lengths
+    prev = torch.cat([torch.ones((1, n), dtype=torch.int64, device="cuda"), cnt[:-1]])
+    d = cnt - prev
+    rs = resets.bool()
+    assert bool((cnt[rs] == 1).all())
+    assert bool((d[~rs].abs() <= 1).all())
+    s = v.state()
+    assert np.array_equal(cnt[-1].cpu().numpy(), s["path_len"].astype(np.int64))
+    assert np.array_equal(pid_t[-1].cpu().numpy(), s["puzzle"].astype(np.int64))

@@ -9,8 +9,9 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "sparc-gym_amd"))
 
-if "--lib" in sys.argv:   # a diagnostic build of the library (set before the package loads it)
-    os.environ["SPARC_DIAG_LIB"] = os.path.abspath(sys.argv[sys.argv.index("--lib") + 1])
+if "--lib" in sys.argv:   # another build of the library, loaded before the package uses it
+    from sparc_gym_amd import _lib as _sparc_lib  # noqa: E402
+    _sparc_lib.load(os.path.abspath(sys.argv[sys.argv.index("--lib") + 1]))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
