@@ -50,6 +50,9 @@ struct Table {
     const uint64_t* __restrict__ init;  // [P] padded W = 1 layout: blocked board at reset
     const uint4* __restrict__ row1;     // [P] padded W = 1 layout: compact puzzle row
     const uint4* __restrict__ trie1;    // [nodes] W = 1 layout: packed nodes (see Env<1>)
+    const uint4* __restrict__ mrow;     // [P] W = 1 split kernel: move-wave row (sparc_split.hpp)
+    const uint4* __restrict__ trow;     // [P] W = 1 split kernel: trie-wave row (sparc_split.hpp)
+    const uint32_t* __restrict__ tab2;  // [nodes][36] W = 1 split kernel: 2-move trie transitions
     uint32_t num_puzzles;
 };
 

@@ -78,16 +78,18 @@ class SparcError(RuntimeError):
     pass
 
 
-def load(path=LIB_PATH):
+def load(path=None):
     """Load and type the HIP library (cached).  Raises if it is missing: no CPU fallback.
 
-    The product path always loads the in-tree build.  Profiling tools may load another build
-    of the same ABI by calling ``load(path)`` themselves before any env is created."""
+    The product path always loads the in-tree build (``path=None``).  Profiling tools may load
+    another build of the same ABI by calling ``load(path)`` themselves before any env is
+    created; later ``load()`` calls then return that library."""
     global _lib
     if _lib is not None:
-        if os.path.abspath(path) != _lib._sparc_path:
+        if path is not None and os.path.abspath(path) != _lib._sparc_path:
             raise ImportError(f"libsparc_gym_amd already loaded from {_lib._sparc_path}")
         return _lib
+    path = LIB_PATH if path is None else path
     if not os.path.exists(path):
         raise ImportError(f"{path} not found: build the HIP extension (make -C sparc-gym_amd)")
     lib = ctypes.CDLL(path)
