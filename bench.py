@@ -41,7 +41,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level par
 # (MI355X_MICROARCH.md, Wave scheduling), at the 2.4 GHz peak engine clock
 VALU_PEAK_WAVE_INSTS = 1024 * 2.4e9 / 2
 CSRC_FILES = ("sparc-gym_amd/csrc/sparc_kernels.hip", "sparc-gym_amd/csrc/sparc_env.hpp",
-              "sparc-gym_amd/csrc/sparc_rules.hpp", "sparc-gym_amd/csrc/sparc_split.hpp", "include/sparc_gym_amd.h", "sparc-gym_amd/Makefile")
+              "sparc-gym_amd/csrc/sparc_rules.hpp", "include/sparc_gym_amd.h", "sparc-gym_amd/Makefile")
 
 CONFIGS = {
     # name: (grid sizes, full property set, traceback, 'new' observation planes every step)

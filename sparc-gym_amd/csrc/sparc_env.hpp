@@ -50,9 +50,6 @@ struct Table {
     const uint64_t* __restrict__ init;  // [P] padded W = 1 layout: blocked board at reset
     const uint4* __restrict__ row1;     // [P] padded W = 1 layout: compact puzzle row
     const uint4* __restrict__ trie1;    // [nodes] W = 1 layout: packed nodes (see Env<1>)
-    const uint4* __restrict__ mrow;     // [P] W = 1 split kernel: move-wave row (sparc_split.hpp)
-    const uint4* __restrict__ trow;     // [P] W = 1 split kernel: trie-wave row (sparc_split.hpp)
-    const uint32_t* __restrict__ tab2;  // [nodes][36] W = 1 split kernel: 2-move trie transitions
     uint32_t num_puzzles;
 };
 
@@ -501,15 +498,8 @@ struct Env<1, TB, Stack> {
     // holds on validated tables; the clamp keeps a broken state from reading out of bounds.
     __device__ __forceinline__ void load_rec(const Params& p) {
         const uint32_t node = nn & 0x7FFFu;
-#ifdef SPARC_DIAG_TRIE_FROM_LDS
-        rec = reinterpret_cast<const uint4*>(diag_lds)[(trie_base + (node < trie_max ? node : trie_max)) & 1023u];
-#else
         rec = p.tab.trie1[trie_base + (node < trie_max ? node : trie_max)];
-#endif
     }
-#ifdef SPARC_DIAG_TRIE_FROM_LDS
-    const uint8_t* diag_lds = nullptr;
-#endif
 
     // _load_puzzle (SPaRC_Gym.py:166-187) with fresh planes: the puzzle rows and the board,
     // not the trie state (inside a rollout the done step's phase_trie runs after this).  The
@@ -624,10 +614,8 @@ struct Env<1, TB, Stack> {
         const bool up = (s_pop != 0u) & on;
         nn = pick(down, c, pick(up, rec.z, nn));
         off = pick(on, s_fwd & (uint32_t)!has, off + s_fwd - s_pop);
-#ifndef SPARC_DIAG_NO_TRIE_LOAD
         // the record changes only with the node (a random walk is off the trie on most steps)
         if (!COND_GATHER || (down | up | (s_rs != 0u))) load_rec(p);
-#endif
         // reward code (1204-1223): done: +100 on a solution, else -100 unless the previous
         // done step already set outcome_reward = 1 (then 0); otherwise +-1 when moved (0 if the
         // puzzle has no solutions); a reset step returns 0 (no move, not done)

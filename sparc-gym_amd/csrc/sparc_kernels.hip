@@ -22,7 +22,6 @@
 
 #include "sparc_env.hpp"
 #include "sparc_rules.hpp"
-#include "sparc_split.hpp"
 #include "sparc_gym_amd.h"
 
 using namespace sparc;
@@ -91,11 +90,7 @@ __device__ __forceinline__ u32x4 nt_load16(const uint8_t* q) {
     return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(q));
 }
 __device__ __forceinline__ void nt_store16(uint8_t* q, u32x4 v) {
-#ifdef SPARC_EXP_STORE_NO_NT
-    *reinterpret_cast<u32x4*>(q) = v;
-#else
     __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(q));
-#endif
 }
 
 // orders one wave's LDS accesses across its lanes (a wave's DS instructions execute in order;
@@ -332,9 +327,6 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
     using Stack = typename std::conditional<(W == 1 && TB), LdsStack<EPW>, RegStack>::type;
     Env<W, TB, Stack> e;
     if constexpr (W == 1 && TB) e.stk.col = smem + kStackOff + wv * (64 * EPW) + lane;
-#ifdef SPARC_DIAG_TRIE_FROM_LDS
-    if constexpr (W == 1) e.diag_lds = smem + kTableOff;
-#endif
     if (active) e.load(p, src, i);
     int4 acc = make_int4(0, 0, 0, 0);
     const uint32_t XY = ot.XD * ot.YD;
@@ -377,26 +369,18 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
                     uint32_t f;
                     const int code = e.advance(p, src, av[j], f);
                     obs(tb + k);
-#ifndef SPARC_DIAG_NO_OUT_LDS
                     tr[k * EPW + lane] = (uint8_t)code;
                     tf[k * EPW + lane] = (uint8_t)f;
-#endif
-#ifdef SPARC_DIAG_NO_STATS
-                    if constexpr (false) {
-#else
                     if constexpr (W == 1) {   // per-step flags the W = 1 step already has
-#endif
                         acc.x += code;
                         acc.y += (int)e.pending;
                         acc.z += (int)e.solved;
                         acc.w += (int)e.was_reset;
                     } else {
-#ifndef SPARC_DIAG_NO_STATS
                         acc.x += code;
                         acc.y += (f & 3u) ? 1 : 0;
                         acc.z += ((f & 3u) && code == 100) ? 1 : 0;
                         acc.w += (f & 64u) ? 1 : 0;
-#endif
                     }
                 }
             }
@@ -508,14 +492,6 @@ __global__ void __launch_bounds__(kBlock1) k_rollout1(Params p, int32_t T, const
                 }
             }
         };
-#if defined(SPARC_DIAG_NO_BARRIER)
-        if (K > 0) load_tile(0);
-        __syncthreads();                                         // B_0
-#elif defined(SPARC_DIAG_IDLE_IO)
-        if (K > 0) load_tile(0);
-        __syncthreads();                                         // B_0
-        for (int32_t k = 0; k < K; ++k) __syncthreads();
-#else
         if (K > 0) load_tile(0);
         __syncthreads();                                         // B_0
         for (int32_t k = 0; k < K; ++k) {
@@ -523,7 +499,6 @@ __global__ void __launch_bounds__(kBlock1) k_rollout1(Params p, int32_t T, const
             if (k >= 2) store_tile(k - 2);
             __syncthreads();                                     // B_{k+1}
         }
-#endif
         __syncthreads();                                         // B_end
         if (K >= 2) store_tile(K - 2);
         if (K >= 1) store_tile(K - 1);
@@ -540,9 +515,6 @@ __global__ void __launch_bounds__(kBlock1) k_rollout1(Params p, int32_t T, const
     using Stack = typename std::conditional<TB, LdsStack<64>, RegStack>::type;
     Env<1, TB, Stack> e;
     if constexpr (TB) e.stk.col = tf + kRing * 64 + lane;
-#ifdef SPARC_DIAG_TRIE_FROM_LDS
-    e.diag_lds = smem + kW1Base;
-#endif
     int4 acc = make_int4(0, 0, 0, 0);
     if (active) {
         e.load(p, src, i);
@@ -570,24 +542,16 @@ __global__ void __launch_bounds__(kBlock1) k_rollout1(Params p, int32_t T, const
                 const int32_t t = k * kTile + g + j;
                 e.reset_next(p, src);
                 const int code = e.phase_trie(p);
-#ifndef SPARC_DIAG_NO_OUT_LDS
                 tr[((t - 1) & (kRing - 1)) * 64 + lane] = (uint8_t)code;   // step t-1 (t = 0: unused row)
-#endif
                 const uint32_t f = e.phase_move(p, av[j]);
-#ifndef SPARC_DIAG_NO_OUT_LDS
                 tf[(t & (kRing - 1)) * 64 + lane] = (uint8_t)f;
-#endif
-#ifndef SPARC_DIAG_NO_STATS
                 acc.x += code;
                 acc.z += (int)e.solved;
                 acc.y += (int)e.pending;
                 acc.w += (int)e.s_rs;
-#endif
             }
         }
-#ifndef SPARC_DIAG_NO_BARRIER
         __syncthreads();                                         // B_{k+1}
-#endif
     }
     if (active) {
         for (int32_t t = K * kTile; t < T; ++t) {                // tail steps / partial workgroups
@@ -709,17 +673,11 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         if (K > 0) load_tile(0);
         __syncthreads();                                         // B_0
         for (int32_t k = 0; k <= K; ++k) {
-#ifdef SPARC_DIAG_SPLIT_IO_IDLE   // timing only: two action tiles reused, no output stores
-            if (k + 1 < K && k < 1) load_tile(k + 1);
-#else
             if (k + 1 < K) load_tile(k + 1);
             if (k >= 2) store_tile(k - 2);
-#endif
             __syncthreads();                                     // B_{k+1}
         }
-#ifndef SPARC_DIAG_SPLIT_IO_IDLE
         if (K >= 1) store_tile(K - 1);
-#endif
         __syncthreads();                                         // B_{K+2}
         return;
     }
@@ -741,12 +699,6 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         __syncthreads();                                         // B_0
         for (int32_t k = 0; k < K; ++k) {
             const uint8_t* ta = pb + kS_Act + (k & 1) * (kTile * 64) + lane;
-#ifdef SPARC_DIAG_SPLIT_MOVE_IDLE
-            if (k >= 0) {
-                __syncthreads();
-                continue;
-            }
-#endif
 #pragma unroll 1
             for (int g = 0; g < kTile; g += 4) {
                 uint32_t av[4];
@@ -784,15 +736,10 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
             stats[i] = st;
         }
     } else {                                                     // ---- trie waves
-#ifndef SPARC_EXP_TRIE_NOPRIO
         // the trie wave wins VALU arbitration against its (older) move wave partner: its chain
         // carries the record-gather waits, the move wave has slack (c3: 0.289 -> 0.266 ms per
         // 1,000 steps; priority to the move wave instead: no change)
         __builtin_amdgcn_s_setprio(1);
-#endif
-#ifdef SPARC_DIAG_TRIE_FROM_LDS
-        e.diag_lds = smem + kS_Base;
-#endif
         e.load_trie(p, src, i);
         if constexpr (!TB) {
             e.npid = e.next_pid(e.pid, p.tab.num_puzzles);
@@ -805,12 +752,6 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         __syncthreads();                                         // B_0
         __syncthreads();                                         // B_1 (interval 0: no tile yet)
         for (int32_t k = 1; k <= K; ++k) {
-#ifdef SPARC_DIAG_SPLIT_TRIE_IDLE
-            if (k >= 0) {
-                __syncthreads();
-                continue;
-            }
-#endif
 #pragma unroll 1
             for (int g = 0; g < kTile; g += 4) {
                 // the group's 4 flag | hand-over words first (one LDS wait), then its 4 steps
@@ -837,243 +778,6 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         fin[0] = make_uint4(e.nn | (e.outcome << 16), e.off, (uint32_t)acc_x, acc_z);
         fin[1] = make_uint4(acc_y, acc_w, 0u, 0u);
         __syncthreads();                                         // B_{K+2}
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
-// W = 1 rollout with each env's step split over THREE waves (k_rollout1r, sparc_split.hpp).
-//
-// Per workgroup 256 envs = 4 pairs of 64; per pair a MOVE wave (0-3), a TRIE wave (4-7) and an
-// I/O wave (8-11), all on the pair's SIMD.  One barrier per 16-step tile; in interval k
-// (between barriers B_k and B_k+1):
-//   move waves   step tile k (decoded actions -> hand-over words)
-//   trie waves   tile k-2 (hand-over words of tiles k-2 and the first of k-1 -> reward codes,
-//                counters)
-//   I/O waves    load + decode the actions of tile k+1; store the reward codes and flags of
-//                tile k-3 (flags = the low bytes of the hand-over words)
-// The hand-over ring holds 4 tiles, the reward codes 2.  Each I/O wave stores rows
-// 8 * (j >> 1) .. + 7 of env half j & 1 (whole 128-B lines, two pairs' row segments).  After
-// the last interval the trie wave hands its final state (node, depth off the trie,
-// outcome_reward, puzzle, counters) to the move wave through LDS, which stores the usual SoA
-// record, so launches chain with every other kernel.  Only full workgroups, T % 16 == 0 and
-// 16-B aligned I/O; the host runs any tail through k_rollout1.
-constexpr int kBlock1r = 768;
-// which roles do their work: bit0 move, bit1 trie, bit2 output stores.  The product build runs
-// all three; `make diag` builds timing-only libraries with roles idled (WRONG results; never
-// loaded by the package) to see which wave sets the time.
-#ifndef SPARC_SPLIT_ROLES
-#define SPARC_SPLIT_ROLES 7
-#endif
-constexpr int kRoles = SPARC_SPLIT_ROLES;
-// the wave role that wins VALU arbitration on its SIMD (s_setprio 1): 1 move, 2 trie, 0 none
-#ifndef SPARC_SPLIT_PRIO
-#define SPARC_SPLIT_PRIO 1
-#endif
-// timing-only diag builds (`make diag`): each wave sums its busy cycles (s_memtime from leaving
-// one barrier to arriving at the next) and writes them, per env, to stats instead of the
-// counters: x move, y trie, z I/O wave, w the whole kernel (move wave)
-#ifndef SPARC_SPLIT_TIMING
-#define SPARC_SPLIT_TIMING 0
-#endif
-struct RoleClock {
-    uint64_t t0 = 0, busy = 0, k0 = 0;
-    __device__ __forceinline__ void begin() {
-        if constexpr (SPARC_SPLIT_TIMING != 0) k0 = t0 = __builtin_readcyclecounter();
-    }
-    __device__ __forceinline__ void start() {
-        if constexpr (SPARC_SPLIT_TIMING != 0) t0 = __builtin_readcyclecounter();
-    }
-    __device__ __forceinline__ void stop() {
-        if constexpr (SPARC_SPLIT_TIMING != 0) busy += __builtin_readcyclecounter() - t0;
-    }
-};
-constexpr int kHwTiles = 4;                             // hand-over ring: tiles k (move) .. k-3 (I/O)
-constexpr size_t kR_Act = 0;                            // decoded actions [2 tiles][16 steps][64] u32
-constexpr size_t kR_HW = kR_Act + 2 * kTile * 64 * 4;   // hand-over ring [4 tiles][16 steps][64] u16
-constexpr size_t kR_Code = kR_HW + kHwTiles * kTile * 64 * 2;   // reward codes [64 steps][64] u8
-constexpr size_t kR_Stk = kR_Code + kRing * 64;         // move stack [64 moves][64] u8 (traceback)
-constexpr size_t kR_Pair = kR_Stk + 64 * 64;
-constexpr size_t kR_Fin = 4 * kR_Pair;                  // final {nn, off, outcome, pid} [256] uint4
-constexpr size_t kR_Stats = kR_Fin + 256 * sizeof(uint4);   // final counters [256] int4
-constexpr size_t kR_Base = kR_Stats + 256 * sizeof(int4);   // staged rows: mrow [2P], trow [P]
-__host__ __device__ constexpr size_t split_table_lds_bytes(uint32_t P) { return (size_t)P * 3 * sizeof(uint4); }
-
-template <bool TB, bool RAND, bool LDS_TABLE>
-__global__ void __launch_bounds__(kBlock1r) k_rollout1r(Params p, int32_t T, const uint8_t* __restrict__ act,
-                                                        uint64_t seed, uint64_t t0, int8_t* __restrict__ rew,
-                                                        uint8_t* __restrict__ flg, int4* __restrict__ stats) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const uint4* mrow = p.tab.mrow;
-    const uint4* trow = p.tab.trow;
-    if constexpr (LDS_TABLE) {
-        const uint32_t P = p.tab.num_puzzles;
-        uint4* lm = reinterpret_cast<uint4*>(smem + kR_Base);
-        uint4* lt = lm + 2 * P;
-        for (uint32_t k = threadIdx.x; k < 2 * P; k += kBlock1r) lm[k] = p.tab.mrow[k];
-        for (uint32_t k = threadIdx.x; k < P; k += kBlock1r) lt[k] = p.tab.trow[k];
-        __syncthreads();
-        mrow = lm;
-        trow = lt;
-    }
-    const size_t n = p.n;
-    const uint32_t wg_base = blockIdx.x * 256u;
-    const int32_t K = T / kTile;
-    const uint32_t pr = wv & 3u;                                 // the pair's 64 envs
-    const uint32_t i = wg_base + pr * 64u + lane;
-    uint8_t* pb = smem + pr * kR_Pair;
-    uint4* fin = reinterpret_cast<uint4*>(smem + kR_Fin) + pr * 64u + lane;
-    int4* fst = reinterpret_cast<int4*>(smem + kR_Stats) + pr * 64u + lane;
-    uint16_t* hwr = reinterpret_cast<uint16_t*>(pb + kR_HW) + lane;
-    RoleClock clk;
-    clk.begin();
-
-    if (wv < 4) {                                                // ---- move waves
-        if constexpr (SPARC_SPLIT_PRIO == 1) __builtin_amdgcn_s_setprio(1);   // the longest chain
-        MoveLane<TB> m;
-        if constexpr (TB) m.stk = pb + kR_Stk + lane;
-        m.load(p, mrow, i);
-        __syncthreads();                                         // B_0
-        for (int32_t k = 0; k < K + 3; ++k) {
-            clk.start();
-            if ((kRoles & 1) && k < K) {
-                const uint32_t* ta = reinterpret_cast<const uint32_t*>(pb + kR_Act) + (k & 1) * (kTile * 64) + lane;
-                uint16_t* hk = hwr + (k % kHwTiles) * (kTile * 64);
-#pragma unroll 1
-                for (int g = 0; g < kTile; g += 4) {
-                    uint32_t av[4];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) av[j] = ta[(g + j) * 64];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) hk[(g + j) * 64] = (uint16_t)m.step_hw(p, mrow, av[j]);
-                }
-            }
-            clk.stop();
-            __syncthreads();                                     // B_{k+1}
-        }
-        __syncthreads();                                         // B_{K+4}: fin / fst complete
-        const uint4 f = fin[0];
-        m.store(p, mrow, i, f.w, f.x, f.y, f.z);
-        if constexpr (SPARC_SPLIT_TIMING != 0) {
-            if (stats) {
-                stats[i].x = (int)clk.busy;
-                stats[i].w = (int)(__builtin_readcyclecounter() - clk.k0);
-            }
-        } else if (stats) {
-            const int4 a = fst[0];
-            int4 st = stats[i];
-            st.x += a.x;
-            st.y += a.y;
-            st.z += a.z;
-            st.w += a.w;
-            stats[i] = st;
-        }
-    } else if (wv < 8) {                                         // ---- trie waves
-        if constexpr (SPARC_SPLIT_PRIO == 2) __builtin_amdgcn_s_setprio(1);
-        TrieLane<TB> t;
-        t.load(p, trow, i);
-        uint8_t* cw = pb + kR_Code + lane;                       // reward code ring [64 steps][64]
-        __syncthreads();                                         // B_0
-        for (int32_t k = 0; k < K + 3; ++k) {
-            clk.start();
-            if ((kRoles & 2) && k >= 1 && k <= K) {
-                const int32_t tt = k - 1;
-                const uint16_t* hk = hwr + (tt % kHwTiles) * (kTile * 64);
-                const uint32_t r0 = (uint32_t)(tt * kTile) & (kRing - 1);
-#pragma unroll 1
-                for (int g = 0; g < kTile; g += 4) {
-                    uint32_t hb[4];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) hb[j] = hk[(g + j) * 64];
-                    // steps t, t+1 emit steps t-2, t-1 (none before the launch's first step)
-                    const bool first = tt == 0 && g == 0;
-                    t.iter(p, trow, hb[0], hb[1], first ? nullptr : cw + ((r0 + g - 2) & (kRing - 1)) * 64,
-                           first ? nullptr : cw + ((r0 + g - 1) & (kRing - 1)) * 64);
-                    t.iter(p, trow, hb[2], hb[3], cw + (r0 + g) * 64, cw + (r0 + g + 1) * 64);
-                }
-                if (tt == K - 1) {                               // the launch's last two steps
-                    const uint2 pr = t.resolve();
-                    cw[((r0 + kTile - 2) & (kRing - 1)) * 64] = (uint8_t)t.emit(t.hwa, pr.x);
-                    cw[((r0 + kTile - 1) & (kRing - 1)) * 64] = (uint8_t)t.emit(t.hwb, pr.y);
-                }
-            }
-            clk.stop();
-            __syncthreads();                                     // B_{k+1}
-        }
-        uint32_t nn, off, pid;
-        t.final_state(trow, t.resolve().y, p.tab.num_puzzles, nn, off, pid);
-        fin[0] = make_uint4(nn, off, t.outcome, pid);
-        if constexpr (SPARC_SPLIT_TIMING != 0) {
-            if (stats) stats[i].y = (int)clk.busy;
-        } else {
-            fst[0] = make_int4(t.acc_x, (int)t.acc_y, (int)t.acc_z, (int)t.acc_w);
-        }
-        __syncthreads();                                         // B_{K+4}
-    } else {                                                     // ---- I/O waves
-        const uint32_t io = pr;
-        const ActionLuts luts = action_luts(p.nbr_pos, p.pitch);
-        const uint32_t r = lane >> 2, c = (lane & 3u) * 16u;     // this lane's piece of an action tile
-        auto fetch_actions = [&](int32_t tt) -> u32x4 {          // raw action bytes of tile tt
-            if constexpr (RAND) {
-                uint32_t v[4] = {0u, 0u, 0u, 0u};
-                const uint64_t g0 = p.env_offset + wg_base + io * 64u + c;
-                const uint64_t tq = t0 + (uint64_t)(tt * kTile + r);
-#pragma unroll
-                for (int j = 0; j < 16; ++j) v[j >> 2] |= uint_rand_action(seed, g0 + j, tq) << ((j & 3) * 8);
-                return u32x4{v[0], v[1], v[2], v[3]};
-            } else {
-                return nt_load16(act + (size_t)(tt * kTile + r) * n + wg_base + io * 64u + c);
-            }
-        };
-        auto put_actions = [&](int32_t tt, u32x4 v) {            // decoded -> buffer tt & 1, row r
-            u32x4* dst = reinterpret_cast<u32x4*>(pb + kR_Act + ((tt & 1) * (kTile * 64) + r * 64 + c) * 4);
-            const uint32_t raw[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                uint32_t o[4];
-                decode_actions4(raw[q], luts, o);
-                dst[q] = u32x4{o[0], o[1], o[2], o[3]};
-            }
-        };
-        auto store_tile = [&](int32_t tt) {                      // codes and flags of tile tt -> HBM
-            const uint32_t r8 = lane >> 3, c8 = (lane & 7u) * 16u;
-            const uint32_t h = io >> 1, q = io & 1u;
-            const uint32_t row = h * 8 + r8;
-            const uint32_t w = 2 * q + (c8 >> 6);
-            const uint8_t* wp = smem + w * kR_Pair;
-            const size_t o = (size_t)(tt * kTile + row) * n + wg_base + q * 128 + c8;
-            if (rew) {
-                const uint8_t* cb = wp + kR_Code + (((tt * kTile) & (kRing - 1)) + row) * 64 + (c8 & 63u);
-                nt_store16(reinterpret_cast<uint8_t*>(rew) + o, *reinterpret_cast<const u32x4*>(cb));
-            }
-            if (flg) {   // the low bytes of 16 u16 hand-over words
-                const uint8_t* fh = wp + kR_HW + (((tt % kHwTiles) * kTile + row) * 64 + (c8 & 63u)) * 2;
-                const u32x4 a = *reinterpret_cast<const u32x4*>(fh);
-                const u32x4 b = *reinterpret_cast<const u32x4*>(fh + 16);
-                u32x4 v;
-                v.x = __builtin_amdgcn_perm(a.y, a.x, 0x06040200u);
-                v.y = __builtin_amdgcn_perm(a.w, a.z, 0x06040200u);
-                v.z = __builtin_amdgcn_perm(b.y, b.x, 0x06040200u);
-                v.w = __builtin_amdgcn_perm(b.w, b.z, 0x06040200u);
-                nt_store16(flg + o, v);
-            }
-        };
-        if (K > 0) put_actions(0, fetch_actions(0));
-        __syncthreads();                                         // B_0
-        for (int32_t k = 0; k < K + 3; ++k) {
-            clk.start();
-            const bool ld = k + 1 < K;
-            u32x4 v = {0u, 0u, 0u, 0u};
-            if (ld) v = fetch_actions(k + 1);                    // in flight during the stores
-            if ((kRoles & 4) && k >= 3) store_tile(k - 3);
-            if (ld) put_actions(k + 1, v);
-            clk.stop();
-            __syncthreads();                                     // B_{k+1}
-        }
-        if constexpr (SPARC_SPLIT_TIMING != 0) {
-            if (stats) stats[i].z = (int)clk.busy;
-        }
-        __syncthreads();                                         // B_{K+4}
     }
 }
 
@@ -1133,9 +837,6 @@ struct Ctx {
     uint4 *t_info = nullptr, *t_root = nullptr, *t_trie = nullptr, *t_trie1 = nullptr;
     uint64_t* t_init = nullptr;
     uint4* t_row1 = nullptr;
-    uint4 *t_mrow = nullptr, *t_trow = nullptr;   // W = 1 split-kernel rows (sparc_split.hpp)
-    uint32_t* t_tab2 = nullptr;                    // W = 1 split kernel: 2-move trie transitions
-    bool split_ok = false;                         // the pool fits the split kernel's packed trie state
     int32_t* err = nullptr;
     uint8_t *s_act = nullptr, *s_flags = nullptr, *s_mask = nullptr;
     int8_t* s_rew = nullptr;
@@ -1192,9 +893,6 @@ Params make_params(const Ctx* c) {
     p.tab.trie1 = c->t_trie1;
     p.tab.init = c->t_init;
     p.tab.row1 = c->t_row1;
-    p.tab.mrow = c->t_mrow;
-    p.tab.trow = c->t_trow;
-    p.tab.tab2 = c->t_tab2;
     p.tab.num_puzzles = c->num_puzzles;
     p.st.vis = c->vis;
     p.st.dirs = c->dirs;
@@ -1314,7 +1012,7 @@ int sparc_destroy(void* ctx) {
     if (!c) return SPARC_OK;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void* bufs[] = {c->vis, c->dirs, c->pos, c->aux, c->step, c->pid, c->t_open, c->t_info, c->t_root, c->t_trie, c->t_trie1, c->t_init, c->t_row1, c->t_mrow, c->t_trow, c->t_tab2,
+    void* bufs[] = {c->vis, c->dirs, c->pos, c->aux, c->step, c->pid, c->t_open, c->t_info, c->t_root, c->t_trie, c->t_trie1, c->t_init, c->t_row1,
                     c->err, c->s_act, c->s_flags, c->s_mask, c->s_rew, c->s_pidx, c->r_planes, c->r_inst_range,
                     c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off, c->s_bits, c->s_region, c->s_fit};
     for (void* b : bufs)
@@ -1410,15 +1108,8 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
     if (c->t_root) HIPCHK(c, hipFree(c->t_root));
     if (c->t_init) HIPCHK(c, hipFree(c->t_init));
     if (c->t_row1) HIPCHK(c, hipFree(c->t_row1));
-    if (c->t_mrow) HIPCHK(c, hipFree(c->t_mrow));
-    if (c->t_trow) HIPCHK(c, hipFree(c->t_trow));
-    if (c->t_tab2) HIPCHK(c, hipFree(c->t_tab2));
-    c->t_tab2 = nullptr;
-    c->split_ok = false;
     c->t_init = nullptr;
     c->t_row1 = nullptr;
-    c->t_mrow = nullptr;
-    c->t_trow = nullptr;
     c->t_open = nullptr;
     c->t_info = nullptr;
     c->t_root = nullptr;
@@ -1493,90 +1184,6 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
         }
         HIPCHK(c, hipMalloc(&c->t_trie1, sizeof(uint4) * nn));
         HIPCHK(c, hipMemcpy(c->t_trie1, t1.data(), sizeof(uint4) * nn, hipMemcpyHostToDevice));
-        // split-kernel rows (sparc_split.hpp): the move wave's {start | target | flags, reset
-        // board}, the trie wave's {trie base, trie max | flags, the root's children}
-        std::vector<uint4> mrow(2 * P), trow(P);
-        // global node index of every packed W = 1 node field (index | terminal << 15) of puzzle q
-        std::vector<uint32_t> qbase(P, 0u);
-        for (size_t q = 0; q < P; ++q) qbase[q] = t->info[4 * q + 2];
-        for (size_t q = 0; q < P; ++q) {
-            const uint32_t* inf = t->info + 4 * q;
-            const bool root = ((inf[1] >> 16) & 2u) != 0u;
-            const uint32_t fl = row1[q].x >> 16;
-            // bk: (len + bk) >> 31 = len >= 3, or len == 2 when the start is open
-            const uint32_t bk = 0x7FFFFFFDu + (((fl >> 2) & 1u) ^ 1u);
-            mrow[2 * q] = make_uint4(row1[q].x & 0xFFu, (row1[q].x >> 8) & 0xFFu, bk,
-                                     (uint32_t)(q + 1 == P ? 0 : q + 1));
-            mrow[2 * q + 1] = make_uint4((uint32_t)init[q], (uint32_t)(init[q] >> 32), 0u, 0u);
-            // the trie wave's packed root state: global root | [start] is a solution << 21 |
-            // depth off the trie (0 when some solution starts at start, else 1) << 22
-            const uint32_t rterm = root ? (t->trie[4 * (size_t)inf[2] + 2] >> 16) & 1u : 0u;
-            const uint32_t rootst = (root ? inf[2] : 0u) | (rterm << kTsTermBit) | ((root ? 0u : 1u) << kTsOffShift) |
-                                    ((fl & 1u) << kTsSolBit);
-            trow[q] = make_uint4(rootst, (uint32_t)(q + 1 == P ? 0 : q + 1), 0u, 0u);
-        }
-        // 2-move transitions (sparc_split.hpp, TrieLane): for every node g (global index) and
-        // move classes (m1, m2) in {forward 0..3, pop, none}, the packed state after m1 then
-        // m2 from (g, off 0).  On the trie a forward move goes to the child or leaves the trie
-        // (off 1), a pop to the parent; off the trie they count the depth.
-        const size_t NN = (size_t)t->num_nodes;
-        c->split_ok = NN <= (size_t)kTsNode + 1;
-        if (c->split_ok) {
-            std::vector<uint32_t> par(NN, 0u), kid(4 * NN, 0xFFFFFFFFu), term(NN, 0u);
-            for (size_t q = 0; q < P; ++q) {
-                const uint32_t* inf = t->info + 4 * q;
-                if (!((inf[1] >> 16) & 2u)) continue;
-                const uint32_t base = inf[2], cnt = inf[3] & 0xFFFFu;
-                for (uint32_t k = 0; k < cnt; ++k) {
-                    const uint32_t* r = t->trie + 4 * ((size_t)base + k);
-                    const uint32_t ch[4] = {r[0] & 0xFFFFu, r[0] >> 16, r[1] & 0xFFFFu, r[1] >> 16};
-                    for (int d = 0; d < 4; ++d)
-                        if (ch[d] != kNone) kid[4 * (base + k) + d] = base + ch[d];
-                    const uint32_t pr = r[2] & 0xFFFFu;
-                    par[base + k] = pr == kNone ? base + k : base + pr;   // the root's "parent": itself (never used)
-                    term[base + k] = (r[2] >> 16) & 1u;
-                }
-            }
-            // which puzzle each node belongs to: its solution flag rides in every packed state
-            std::vector<uint32_t> nsol(NN, 0u);
-            for (size_t q = 0; q < P; ++q) {
-                const uint32_t* inf = t->info + 4 * q;
-                if (!((inf[1] >> 16) & 2u)) continue;
-                for (uint32_t k = 0; k < (inf[3] & 0xFFFFu); ++k) nsol[inf[2] + k] = (inf[1] >> 16) & 1u;
-            }
-            auto pack = [&](uint32_t g, uint32_t off) {
-                return g | (term[g] << kTsTermBit) | (off << kTsOffShift) | (nsol[g] << kTsSolBit);
-            };
-            auto apply = [&](uint32_t& g, uint32_t& off, uint32_t m) {
-                if (m == kClsN) return;
-                if (m == kClsB) {
-                    if (off) --off;
-                    else g = par[g];
-                    return;
-                }
-                if (off) ++off;
-                else if (kid[4 * g + m] != 0xFFFFFFFFu) g = kid[4 * g + m];
-                else off = 1;
-            };
-            // entry (g, m1, m2) = {state after m1, state after m1 then m2}, from (g, off 0)
-            std::vector<uint32_t> tab2(std::max<size_t>(NN, 1) * kTab2Row * 2, 0u);
-            for (size_t g0 = 0; g0 < NN; ++g0)
-                for (uint32_t m1 = 0; m1 < kClasses; ++m1)
-                    for (uint32_t m2 = 0; m2 < kClasses; ++m2) {
-                        uint32_t g = (uint32_t)g0, off = 0;
-                        apply(g, off, m1);
-                        const size_t e = 2 * (g0 * kTab2Row + m1 * kClasses + m2);
-                        tab2[e] = pack(g, off);
-                        apply(g, off, m2);
-                        tab2[e + 1] = pack(g, off);
-                    }
-            HIPCHK(c, hipMalloc(&c->t_tab2, sizeof(uint32_t) * tab2.size()));
-            HIPCHK(c, hipMemcpy(c->t_tab2, tab2.data(), sizeof(uint32_t) * tab2.size(), hipMemcpyHostToDevice));
-        }
-        HIPCHK(c, hipMalloc(&c->t_mrow, sizeof(uint4) * 2 * P));
-        HIPCHK(c, hipMalloc(&c->t_trow, sizeof(uint4) * P));
-        HIPCHK(c, hipMemcpy(c->t_mrow, mrow.data(), sizeof(uint4) * 2 * P, hipMemcpyHostToDevice));
-        HIPCHK(c, hipMemcpy(c->t_trow, trow.data(), sizeof(uint4) * P, hipMemcpyHostToDevice));
     }
     c->num_puzzles = (uint32_t)t->num_puzzles;
     c->num_nodes = (uint32_t)t->num_nodes;
@@ -1674,40 +1281,25 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
         const size_t per_cu = (blocks + 255) / 256;
         const size_t budget = std::min(kMaxDynLds, (size_t)160 * 1024 / (per_cu ? per_cu : 1));
         const size_t tbytes = table_lds_bytes<1>(c->num_puzzles);
-#ifndef SPARC_EXP_NO_SPLIT
         // the full tiles of full workgroups go through the split move / trie kernel (MI355X, c3
         // at 65,536 envs: 0.266 vs 0.312 ms per 1,000 steps); a tail of T % 16 steps or a batch
         // that is not a multiple of 256 envs goes through k_rollout1 below
-        if (tiled && c->n % 256 == 0 && T >= kTile && (c->split_ok || getenv("SPARC_OLD_SPLIT"))) {
+        if (tiled && c->n % 256 == 0 && T >= kTile) {
             const int32_t T16 = T / kTile * kTile;
-            static const bool old_split = getenv("SPARC_OLD_SPLIT") != nullptr;   // A/B during development
-            const size_t sbase = old_split ? kS_Base : kR_Base;
-            const size_t stab = old_split ? tbytes : split_table_lds_bytes(c->num_puzzles);
-            const bool lds_s = sbase + stab <= budget;
-            const size_t shm_s = sbase + (lds_s ? stab : 0);
-            const int blk = old_split ? kBlock1s : kBlock1r;
+            const bool lds_s = kS_Base + tbytes <= budget;
+            const size_t shm_s = kS_Base + (lds_s ? tbytes : 0);
             auto launch_s = [&](auto kern, const uint8_t* a) {
                 if (shm_s > 64 * 1024 && (lds_rc = allow_big_lds(c, reinterpret_cast<const void*>(kern)))) return;
-                kern<<<dim3((unsigned)blocks), blk, shm_s, c->stream>>>(p, T16, a, seed, t0, d_rew, d_flags, st);
+                kern<<<dim3((unsigned)blocks), kBlock1s, shm_s, c->stream>>>(p, T16, a, seed, t0, d_rew, d_flags, st);
             };
             auto go_s = [&](auto tb) {
                 constexpr bool TB = decltype(tb)::value;
-                if (old_split) {
-                    if (d_act) {
-                        if (lds_s) launch_s(k_rollout1s<TB, false, true>, d_act);
-                        else launch_s(k_rollout1s<TB, false, false>, d_act);
-                    } else {
-                        if (lds_s) launch_s(k_rollout1s<TB, true, true>, nullptr);
-                        else launch_s(k_rollout1s<TB, true, false>, nullptr);
-                    }
-                    return;
-                }
                 if (d_act) {
-                    if (lds_s) launch_s(k_rollout1r<TB, false, true>, d_act);
-                    else launch_s(k_rollout1r<TB, false, false>, d_act);
+                    if (lds_s) launch_s(k_rollout1s<TB, false, true>, d_act);
+                    else launch_s(k_rollout1s<TB, false, false>, d_act);
                 } else {
-                    if (lds_s) launch_s(k_rollout1r<TB, true, true>, nullptr);
-                    else launch_s(k_rollout1r<TB, true, false>, nullptr);
+                    if (lds_s) launch_s(k_rollout1s<TB, true, true>, nullptr);
+                    else launch_s(k_rollout1s<TB, true, false>, nullptr);
                 }
             };
             if (c->cfg.traceback) go_s(std::true_type{});
@@ -1722,7 +1314,6 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
             t0 += (uint64_t)T16;
             T -= T16;
         }
-#endif
         const bool lds_table = kW1Base + tbytes <= budget;
         const size_t shm = kW1Base + (lds_table ? tbytes : 0);
         auto launch = [&](auto kern, const uint8_t* a) {

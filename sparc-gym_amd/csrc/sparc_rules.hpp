@@ -329,9 +329,7 @@ __device__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const BB<W>& vi
         }
         if (has) {
             bool ok = Rc.popc() == pa - ya;
-#ifndef SPARC_DIAG_RULES_NO_FIT
             if (ok) ok = exact_fit<W>(fin, Rc, P, p.err);
-#endif
             if (ok) fit_ok |= 1ull << (rid & 63);
             poly_ok &= ok;
         }

@@ -30,8 +30,6 @@ ap.add_argument("--rand", action="store_true", help="in-kernel counter-based act
 ap.add_argument("--no-out", action="store_true", help="do not write reward codes / flags")
 ap.add_argument("--time", action="store_true", help="print the mean launch time (HIP events)")
 ap.add_argument("--lib", default=None, help="path of a diagnostic build of libsparc_gym_amd.so")
-ap.add_argument("--timing", action="store_true",
-                help="the --lib build writes per-role busy cycles into stats (make diag, SPARC_SPLIT_TIMING)")
 a = ap.parse_args()
 sizes, full, tb, obs = bench.CONFIGS[a.config]
 proc = process_puzzles(synthetic.make_puzzles(1024, seed=0, sizes=sizes, full_properties=full))
@@ -59,13 +57,6 @@ for k in range(a.launches + 1):      # first launch = warmup
     e1.record()
     ms.append((e0, e1))
 torch.cuda.synchronize()
-if a.timing:   # last launch: per-role busy cycles (move, trie, reward) and the whole kernel
-    st = stats.cpu().numpy().astype(np.float64)
-    K = a.chunk // 16
-    names = ("move", "trie", "reward", "kernel")
-    print("role cycles per 16-step tile: " + "  ".join(
-        f"{nm} {st[:, j].mean() / K:.0f} (max {st[:, j].max() / K:.0f})" for j, nm in enumerate(names)))
-    print("role cycles per env-step:     " + "  ".join(f"{nm} {st[:, j].mean() / (16 * K):.1f}" for j, nm in enumerate(names)))
 if a.time:
     t = [x.elapsed_time(y) for x, y in ms[1:]]
     print(f"rollout ms/launch {sum(t) / len(t):.4f}  env-steps/s {a.envs * a.chunk / (sum(t) / len(t) / 1e3):.4e}"
