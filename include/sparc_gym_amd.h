@@ -235,7 +235,11 @@ enum {
     SPARC_RULE_STAR_PAIRING = 1 << 5,         /* 553-619                             */
     SPARC_RULE_TRIANGLES = 1 << 6,            /* 622-646                             */
     SPARC_RULE_POLY_YLOP = 1 << 7,            /* 648-838                             */
-    SPARC_RULE_ALL = 1 << 8                   /* all_rules_satisfied 931-936         */
+    SPARC_RULE_ALL = 1 << 8,                  /* all_rules_satisfied 931-936         */
+    /* not a rule: an exact-fit search of this env (_polyfit_region_exact, 738-853) passed 2^26
+     * nodes without an answer; its poly/ylop bit (and ALL) then read 0, and the host refuses to
+     * build that env's rule_status.  The reference has no cap; no pool of this repo reaches it. */
+    SPARC_RULE_SEARCH_EXHAUSTED = 1 << 9
 };
 
 /* Load the rule table (host arrays, copied).  Call after sparc_load_puzzles, which drops it. */

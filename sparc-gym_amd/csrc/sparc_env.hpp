@@ -50,10 +50,6 @@ struct Table {
     const uint64_t* __restrict__ init;  // [P] padded W = 1 layout: blocked board at reset
     const uint4* __restrict__ row1;     // [P] padded W = 1 layout: compact puzzle row
     const uint4* __restrict__ trie1;    // [nodes] W = 1 layout: packed nodes (see Env<1>)
-    const uint2* __restrict__ mblk;     // [P][mrows][4] W = 1 split kernel: leaf-set masks (sparc_mask.hpp)
-    const uint16_t* __restrict__ nodeof;   // [leaves][mrows] node of each leaf's path at each depth
-    const uint32_t* __restrict__ leafset;  // [nodes] leaves below each node
-    uint32_t mrows;                     // rows per mask block (0: the pool has no mask table)
     uint32_t num_puzzles;
 };
 
@@ -557,8 +553,9 @@ struct Env<1, TB, Stack> {
     }
 
     // reset_next with the next puzzle's row word and board already in registers: they were read
-    // from LDS at the previous reset (or at load), so a reset waits on no LDS read; a resetting
-    // lane then reads the rows of the puzzle after the new one for its next reset
+    // from LDS at the previous reset (or at load), so a reset waits on no LDS read (MI355X, c3:
+    // 0.466 -> 0.460 ms per 2,000-step launch); a resetting lane then reads the rows of the
+    // puzzle after the new one, for its next reset
     template <class Src>
     __device__ __forceinline__ void prefetch_reset(const Src& src, uint32_t num_puzzles) {
         rpid = pid + 1 == num_puzzles ? 0u : pid + 1;
@@ -672,15 +669,14 @@ struct Env<1, TB, Stack> {
 
     // ---- k_rollout1s: the step split over a move wave (reset_next + phase_move) and a trie
     // wave (phase_trie).  The move wave hands each step over as one 16-bit LDS word: its flag
-    // byte f (term | trunc << 1 | legal << 2 | reset << 6) | (1 + forward - pop) << 8 | action
+    // byte f (term | trunc << 1 | legal << 2 | reset << 6) | pop << 8 | forward << 9 | action
     // << 10.  The trie wave derives done (f & 3), the reset step (bit 6) and
     // moved-with-solutions (forward or pop, on a puzzle with solutions) from it, so the move
-    // wave's serial chain only packs three fields; bits 8-9 are the change of len(self.path)
-    // plus one (0 pop, 1 none, 2 forward).  An action >= 4 never moves (forward = pop = 0); its
-    // bits above 15 are cut by the 16-bit store, and the trie wave reads only action & 3, which
-    // the cut keeps.  The I/O wave stores the low bytes as the flag output.
+    // wave's serial chain only packs three fields.  An action >= 4 never moves (forward = pop
+    // = 0); its bits above 15 are cut by the 16-bit store, and the trie wave reads only
+    // action & 3, which the cut keeps.  The I/O wave stores the low bytes as the flag output.
     __device__ __forceinline__ uint32_t hand_word(uint32_t f) const {
-        return (((s_a << 2) + 1u + s_fwd - s_pop) << 8) | f;
+        return (((((s_a << 1) | s_fwd) << 1) | s_pop) << 8) | f;
     }
     // the trie wave's side: unpack the word; a reset step moves to the next puzzle's rows, as
     // the move wave's reset_next did for its part (index + 1 mod P, SPaRC_Gym.py:1087), and
@@ -688,7 +684,7 @@ struct Env<1, TB, Stack> {
     template <class Src>
     __device__ __forceinline__ void take_hand_word(const Src& src, uint32_t num_puzzles, uint32_t hw) {
         s_rs = (hw >> 6) & 1u;
-        s_pop = TB ? (uint32_t)((hw & 0x300u) == 0u) : 0u;   // no pops without traceback
+        s_pop = TB ? (hw >> 8) & 1u : 0u;   // no pops without traceback
         s_fwd = (hw >> 9) & 1u;
         s_a = (hw >> 10) & 3u;
         s_done = (uint32_t)((hw & 3u) != 0u);
@@ -717,7 +713,7 @@ struct Env<1, TB, Stack> {
     template <class Src>
     __device__ __forceinline__ void take_hand_word_pf(const Src& src, uint32_t num_puzzles, uint32_t hw) {
         s_rs = (hw >> 6) & 1u;
-        s_pop = TB ? (uint32_t)((hw & 0x300u) == 0u) : 0u;
+        s_pop = TB ? (hw >> 8) & 1u : 0u;
         s_fwd = (hw >> 9) & 1u;
         s_a = (hw >> 10) & 3u;
         s_done = (uint32_t)((hw & 3u) != 0u);

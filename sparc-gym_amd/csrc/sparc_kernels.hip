@@ -21,7 +21,6 @@
 #include <vector>
 
 #include "sparc_env.hpp"
-#include "sparc_mask.hpp"
 #include "sparc_rules.hpp"
 #include "sparc_gym_amd.h"
 
@@ -611,24 +610,17 @@ constexpr size_t kS_Stk = kS_FH + 2 * kRing * 64;     // move stack [64 moves][6
 constexpr size_t kS_Pair = kS_Stk + 64 * 64;          // per move / trie wave pair
 constexpr size_t kS_Fin = 4 * kS_Pair;                // trie wave's final state [4][64] 2 x uint4
 constexpr size_t kS_Base = kS_Fin + 4 * 64 * 2 * sizeof(uint4);
-// leaf-set trie waves with traceback (TM > 0, sparc_mask.hpp): a [mrows + 2][64] u32 stack of
-// the sets along the path per pair, after kS_Base; the staged puzzle rows follow it
-__host__ __device__ constexpr size_t mask_stack_lds_bytes(uint32_t mrows) { return (size_t)4 * (mrows + 2) * 256; }
 
-// TM: the trie wave's formulation.  0: node trie (Env<1>::phase_trie, one record gather per
-// on-trie step, on the chain); 1 / 2: leaf sets (MaskTrie; 2 = next-step autoreset), used when
-// the pool has a mask table (every puzzle <= 31 trie leaves).
-template <bool TB, bool RAND, bool LDS_TABLE, int TM>
+template <bool TB, bool RAND, bool LDS_TABLE>
 __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, const uint8_t* __restrict__ act,
                                                         uint64_t seed, uint64_t t0, int8_t* __restrict__ rew,
                                                         uint8_t* __restrict__ flg, int4* __restrict__ stats) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const size_t tab_off = kS_Base + ((TM > 0 && TB) ? mask_stack_lds_bytes(p.tab.mrows) : 0);
     PuzzleSrc<1> src{p.tab.info, p.tab.root, p.tab.open, p.tab.init, p.tab.row1};
     if constexpr (LDS_TABLE) {
         const uint32_t P = p.tab.num_puzzles;
-        uint4* lrow1 = reinterpret_cast<uint4*>(smem + tab_off);
+        uint4* lrow1 = reinterpret_cast<uint4*>(smem + kS_Base);
         uint64_t* linit = reinterpret_cast<uint64_t*>(lrow1 + P);
         for (uint32_t k = threadIdx.x; k < P; k += kBlock1s) {
             lrow1[k] = p.tab.row1[k];
@@ -744,25 +736,7 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
             st.w += (int)(fc.y + acc_w);
             stats[i] = st;
         }
-    } else if constexpr (TM > 0) {                               // ---- trie waves, leaf sets
-        MaskTrie<TB, TM == 2> mt;
-        if constexpr (TB) mt.stk = smem + kS_Base + (size_t)pr * (p.tab.mrows + 2) * 256 + lane * 4u;
-        mt.load(p, src, i);
-        const uint16_t* th = reinterpret_cast<const uint16_t*>(pb + kS_FH) + lane;
-        uint8_t* tr = pb + kS_Rew + lane;
-        __syncthreads();                                         // B_0
-        __syncthreads();                                         // B_1 (interval 0: no tile yet)
-        for (int32_t k = 1; k <= K; ++k) {
-            const uint32_t row0 = (uint32_t)((k - 1) * kTile) & (kRing - 1);
-            mt.tile(th + row0 * 64, tr + row0 * 64);
-            __syncthreads();                                     // B_{k+1}
-        }
-        uint32_t nn, oc;
-        mt.final_state(p, src, nn, oc);
-        fin[0] = make_uint4(nn | (oc << 16), mt.off, (uint32_t)mt.acc_x, mt.acc_z);
-        fin[1] = make_uint4(mt.acc_y, mt.acc_w, 0u, 0u);
-        __syncthreads();                                         // B_{K+2}
-    } else {                                                     // ---- trie waves, node trie
+    } else {                                                     // ---- trie waves
         // the trie wave wins VALU arbitration against its (older) move wave partner: its chain
         // carries the record-gather waits, the move wave has slack (c3: 0.289 -> 0.266 ms per
         // 1,000 steps; priority to the move wave instead: no change)
@@ -864,11 +838,6 @@ struct Ctx {
     uint4 *t_info = nullptr, *t_root = nullptr, *t_trie = nullptr, *t_trie1 = nullptr;
     uint64_t* t_init = nullptr;
     uint4* t_row1 = nullptr;
-    // leaf-set tables of the k_rollout1s trie wave (sparc_mask.hpp); mrows = 0: not built
-    uint2* t_mblk = nullptr;
-    uint16_t* t_nodeof = nullptr;
-    uint32_t* t_leafset = nullptr;
-    uint32_t mrows = 0;
     int32_t* err = nullptr;
     uint8_t *s_act = nullptr, *s_flags = nullptr, *s_mask = nullptr;
     int8_t* s_rew = nullptr;
@@ -925,10 +894,6 @@ Params make_params(const Ctx* c) {
     p.tab.trie1 = c->t_trie1;
     p.tab.init = c->t_init;
     p.tab.row1 = c->t_row1;
-    p.tab.mblk = c->t_mblk;
-    p.tab.nodeof = c->t_nodeof;
-    p.tab.leafset = c->t_leafset;
-    p.tab.mrows = c->mrows;
     p.tab.num_puzzles = c->num_puzzles;
     p.st.vis = c->vis;
     p.st.dirs = c->dirs;
@@ -983,95 +948,6 @@ int check_ctx(Ctx* c, bool need_state) {
 
 int launch_check(Ctx* c) {
     HIPCHK(c, hipGetLastError());
-    return SPARC_OK;
-}
-
-// Leaf-set tables of the k_rollout1s trie wave (layout: sparc_mask.hpp), built from the validated
-// node tries.  Leaves of puzzle q are its trie nodes without children, numbered in node order;
-// every puzzle must have <= kMaskLeaves of them (else mrows stays 0 and the node-trie wave runs).
-// mblk[q][i][d] = {M(i - 1, d), E(i)}, row 0 = {A0, E(0) | has_solutions << 31};
-// nodeof[(leafbase(q) + l) * R + k] = the depth-k node on leaf l's path; leafset[node] = the
-// leaves below it.  row1[q].w = leafbase(q).
-int build_mask_tables(Ctx* c, const sparc_puzzle_table* t, std::vector<uint4>& row1) {
-    const size_t P = (size_t)t->num_puzzles, NN = (size_t)(t->num_nodes > 0 ? t->num_nodes : 0);
-    std::vector<uint32_t> leafset(std::max<size_t>(NN, 1), 0u), leafbase(P, 0u);
-    std::vector<std::vector<uint32_t>> leaves(P);   // global node ids of each puzzle's leaves
-    uint32_t dmax = 0, nleaves = 0;
-    auto rec = [&](size_t g) { return t->trie + 4 * g; };
-    for (size_t q = 0; q < P; ++q) {
-        const uint32_t* inf = t->info + 4 * q;
-        leafbase[q] = nleaves;
-        if (!((inf[1] >> 16) & 2u)) continue;
-        const uint32_t base = inf[2], cnt = inf[3] & 0xFFFFu;
-        std::vector<uint32_t> depth(cnt, 0u);
-        for (uint32_t k = 0; k < cnt; ++k) {
-            const uint32_t* r = rec(base + k);
-            if (k > 0) {
-                const uint32_t par = r[2] & 0xFFFFu;
-                if (par >= k) return SPARC_OK;   // not parent-before-child: no mask table
-                depth[k] = depth[par] + 1u;
-            }
-            const bool leaf = r[0] == 0xFFFFFFFFu && r[1] == 0xFFFFFFFFu;
-            if (leaf) {
-                if (leaves[q].size() == kMaskLeaves) return SPARC_OK;   // too many: no mask table
-                leafset[base + k] = 1u << leaves[q].size();
-                leaves[q].push_back(base + k);
-                dmax = std::max(dmax, depth[k]);
-            }
-        }
-        // parents have lower indices than their children (build_trie appends): one reverse pass
-        for (uint32_t k = cnt; k-- > 1;) {
-            const uint32_t par = rec(base + k)[2] & 0xFFFFu;
-            leafset[base + par] |= leafset[base + k];
-        }
-        nleaves += (uint32_t)leaves[q].size();
-    }
-    if (dmax > 61) return SPARC_OK;   // paths of a 64-bit board have <= 63 points
-    const uint32_t R = dmax + 2;
-    std::vector<uint2> mblk((P + 16) * R * 4, make_uint2(0u, 0u));   // + 16 wrap-around copies
-    std::vector<uint16_t> nodeof(std::max<size_t>((size_t)nleaves * R, 1), 0u);
-    for (size_t q = 0; q < P; ++q) {
-        const uint32_t* inf = t->info + 4 * q;
-        uint2* b = mblk.data() + q * R * 4;
-        const uint32_t hs = (inf[1] >> 16) & 1u;
-        const bool root = ((inf[1] >> 16) & 2u) != 0u;
-        const uint32_t base = inf[2];
-        const uint32_t a0 = root ? leafset[base] : 0u;
-        const uint32_t e0 = (root && ((rec(base)[2] >> 16) & 1u)) ? a0 : 0u;
-        for (int d = 0; d < 4; ++d) b[d] = make_uint2(a0, e0 | (hs << 31));
-        for (size_t l = 0; l < leaves[q].size(); ++l) {
-            // the leaf's path, root first
-            std::vector<uint32_t> path;
-            for (uint32_t g = leaves[q][l];; g = base + (rec(g)[2] & 0xFFFFu)) {
-                path.push_back(g);
-                if (g == base) break;
-            }
-            std::reverse(path.begin(), path.end());
-            const uint32_t bit = 1u << l;
-            for (size_t k = 0; k < path.size(); ++k) {
-                nodeof[(size_t)(leafbase[q] + l) * R + k] = (uint16_t)(path[k] - base);
-                if (k > 0) {
-                    const uint32_t* pr = rec(path[k - 1]);
-                    const uint32_t ch[4] = {pr[0] & 0xFFFFu, pr[0] >> 16, pr[1] & 0xFFFFu, pr[1] >> 16};
-                    int d = 0;
-                    while (d < 4 && base + ch[d] != path[k]) ++d;
-                    b[k * 4 + d].x |= bit;                      // M(k - 1, d)
-                }
-                if ((rec(path[k])[2] >> 16) & 1u)
-                    for (int d = 0; d < 4; ++d) b[k * 4 + d].y |= bit;   // E(k)
-            }
-        }
-        row1[q].w = leafbase[q];
-    }
-    for (size_t q = P; q < P + 16; ++q)
-        std::copy_n(mblk.data() + (q % P) * R * 4, R * 4, mblk.data() + q * R * 4);
-    HIPCHK(c, hipMalloc(&c->t_mblk, sizeof(uint2) * mblk.size()));
-    HIPCHK(c, hipMemcpy(c->t_mblk, mblk.data(), sizeof(uint2) * mblk.size(), hipMemcpyHostToDevice));
-    HIPCHK(c, hipMalloc(&c->t_nodeof, sizeof(uint16_t) * nodeof.size()));
-    HIPCHK(c, hipMemcpy(c->t_nodeof, nodeof.data(), sizeof(uint16_t) * nodeof.size(), hipMemcpyHostToDevice));
-    HIPCHK(c, hipMalloc(&c->t_leafset, sizeof(uint32_t) * leafset.size()));
-    HIPCHK(c, hipMemcpy(c->t_leafset, leafset.data(), sizeof(uint32_t) * leafset.size(), hipMemcpyHostToDevice));
-    c->mrows = R;
     return SPARC_OK;
 }
 
@@ -1137,7 +1013,7 @@ int sparc_destroy(void* ctx) {
     if (!c) return SPARC_OK;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void* bufs[] = {c->vis, c->dirs, c->pos, c->aux, c->step, c->pid, c->t_open, c->t_info, c->t_root, c->t_trie, c->t_trie1, c->t_init, c->t_row1, c->t_mblk, c->t_nodeof, c->t_leafset,
+    void* bufs[] = {c->vis, c->dirs, c->pos, c->aux, c->step, c->pid, c->t_open, c->t_info, c->t_root, c->t_trie, c->t_trie1, c->t_init, c->t_row1,
                     c->err, c->s_act, c->s_flags, c->s_mask, c->s_rew, c->s_pidx, c->r_planes, c->r_inst_range,
                     c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off, c->s_bits, c->s_region, c->s_fit};
     for (void* b : bufs)
@@ -1174,7 +1050,6 @@ int sparc_sync(void* ctx) {
     if (e) {
         HIPCHK(c, hipMemset(c->err, 0, sizeof(int32_t)));
         if (e & 2) return fail(c, SPARC_E_STATE, "device-side trie node out of range (state corrupted)");
-        if (e & 4) return fail(c, SPARC_E_STATE, "rule audit: exact-fit search exceeded 2^26 nodes");
         if (e & 8) return fail(c, SPARC_E_STATE, "rule audit: env puzzle index outside the rule table");
         return fail(c, SPARC_E_INVALID, "device-side puzzle index out of range in a reset");
     }
@@ -1233,13 +1108,6 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
     if (c->t_root) HIPCHK(c, hipFree(c->t_root));
     if (c->t_init) HIPCHK(c, hipFree(c->t_init));
     if (c->t_row1) HIPCHK(c, hipFree(c->t_row1));
-    if (c->t_mblk) HIPCHK(c, hipFree(c->t_mblk));
-    if (c->t_nodeof) HIPCHK(c, hipFree(c->t_nodeof));
-    if (c->t_leafset) HIPCHK(c, hipFree(c->t_leafset));
-    c->t_mblk = nullptr;
-    c->t_nodeof = nullptr;
-    c->t_leafset = nullptr;
-    c->mrows = 0;
     c->t_init = nullptr;
     c->t_row1 = nullptr;
     c->t_open = nullptr;
@@ -1293,6 +1161,8 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
                                  inf[2], (cnt ? cnt - 1u : 0u) | (legal0 << 16), 0u);
         }
     }
+    HIPCHK(c, hipMalloc(&c->t_row1, sizeof(uint4) * P));
+    HIPCHK(c, hipMemcpy(c->t_row1, row1.data(), sizeof(uint4) * P, hipMemcpyHostToDevice));
     HIPCHK(c, hipMalloc(&c->t_init, sizeof(uint64_t) * P));
     HIPCHK(c, hipMemcpy(c->t_info, dinfo.data(), sizeof(uint4) * P, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->t_init, init.data(), sizeof(uint64_t) * P, hipMemcpyHostToDevice));
@@ -1314,12 +1184,7 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
         }
         HIPCHK(c, hipMalloc(&c->t_trie1, sizeof(uint4) * nn));
         HIPCHK(c, hipMemcpy(c->t_trie1, t1.data(), sizeof(uint4) * nn, hipMemcpyHostToDevice));
-        int rc = build_mask_tables(c, t, row1);
-        if (rc) return rc;
     }
-    // row1 last: build_mask_tables puts each puzzle's first leaf id in row1[q].w
-    HIPCHK(c, hipMalloc(&c->t_row1, sizeof(uint4) * P));
-    HIPCHK(c, hipMemcpy(c->t_row1, row1.data(), sizeof(uint4) * P, hipMemcpyHostToDevice));
     c->num_puzzles = (uint32_t)t->num_puzzles;
     c->num_nodes = (uint32_t)t->num_nodes;
     c->loaded = true;
@@ -1421,35 +1286,24 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
         // that is not a multiple of 256 envs goes through k_rollout1 below
         if (tiled && c->n % 256 == 0 && T >= kTile) {
             const int32_t T16 = T / kTile * kTile;
-            // the leaf-set trie wave when the pool has its tables (and, with traceback, its path
-            // stack fits next to the I/O rings)
-            const size_t mstk = c->cfg.traceback ? mask_stack_lds_bytes(c->mrows) : 0;
-            const int tm = (c->mrows > 0 && kS_Base + mstk <= kMaxDynLds) ? (c->cfg.autoreset ? 2 : 1) : 0;
-            const size_t sbase = kS_Base + (tm ? mstk : 0);
-            const bool lds_s = sbase + tbytes <= budget;
-            const size_t shm_s = sbase + (lds_s ? tbytes : 0);
+            const bool lds_s = kS_Base + tbytes <= budget;
+            const size_t shm_s = kS_Base + (lds_s ? tbytes : 0);
             auto launch_s = [&](auto kern, const uint8_t* a) {
                 if (shm_s > 64 * 1024 && (lds_rc = allow_big_lds(c, reinterpret_cast<const void*>(kern)))) return;
                 kern<<<dim3((unsigned)blocks), kBlock1s, shm_s, c->stream>>>(p, T16, a, seed, t0, d_rew, d_flags, st);
             };
-            auto go_s = [&](auto tb, auto tmc) {
+            auto go_s = [&](auto tb) {
                 constexpr bool TB = decltype(tb)::value;
-                constexpr int TM = decltype(tmc)::value;
                 if (d_act) {
-                    if (lds_s) launch_s(k_rollout1s<TB, false, true, TM>, d_act);
-                    else launch_s(k_rollout1s<TB, false, false, TM>, d_act);
+                    if (lds_s) launch_s(k_rollout1s<TB, false, true>, d_act);
+                    else launch_s(k_rollout1s<TB, false, false>, d_act);
                 } else {
-                    if (lds_s) launch_s(k_rollout1s<TB, true, true, TM>, nullptr);
-                    else launch_s(k_rollout1s<TB, true, false, TM>, nullptr);
+                    if (lds_s) launch_s(k_rollout1s<TB, true, true>, nullptr);
+                    else launch_s(k_rollout1s<TB, true, false>, nullptr);
                 }
             };
-            auto go_tm = [&](auto tb) {
-                if (tm == 2) go_s(tb, std::integral_constant<int, 2>{});
-                else if (tm == 1) go_s(tb, std::integral_constant<int, 1>{});
-                else go_s(tb, std::integral_constant<int, 0>{});
-            };
-            if (c->cfg.traceback) go_tm(std::true_type{});
-            else go_tm(std::false_type{});
+            if (c->cfg.traceback) go_s(std::true_type{});
+            else go_s(std::false_type{});
             if (lds_rc) return lds_rc;
             rc = launch_check(c);
             if (rc || T16 == T) return rc;

@@ -32,7 +32,7 @@
 
 namespace sparc {
 
-constexpr uint32_t kErrRuleSearch = 4, kErrRuleTable = 8;
+constexpr uint32_t kErrRuleTable = 8;
 // rule-plane indices of include/sparc_gym_amd.h (SPARC_RULE_PLANES)
 enum : uint32_t {
     RP_CELLS = 0, RP_LATTICE, RP_GAPS, RP_DOTS, RP_TRI, RP_TRI0, RP_TRI1, RP_TRI2, RP_STAR, RP_SQUARE,
@@ -42,7 +42,7 @@ constexpr int kFitCells = 64;     // cell grid of the exact fit (15 x 15 lattice
 constexpr int kFitYlops = 16;     // per puzzle limits, validated by the loader
 constexpr int kFitShapes = 16;
 constexpr int kFitDepth = 64;
-constexpr uint32_t kFitCap = 1u << 26;   // search nodes before a loud failure (kErrRuleSearch)
+constexpr uint32_t kFitCap = 1u << 26;   // search nodes before the env's audit reports SPARC_RULE_SEARCH_EXHAUSTED
 
 struct RulesTab {
     const uint64_t* __restrict__ planes;      // [P][RP_COUNT][W]
@@ -148,9 +148,11 @@ __device__ __forceinline__ void fit_shape(const RulesTab& rt, uint32_t sh, uint3
 
 // _polyfit_region_exact with the area check passed (so net = area > 0 and the grid starts at
 // -1 on the region's cells), as a depth-first search over the same choices (existence only:
-// identical ylops take non-decreasing anchors, polys are tried by distinct shape)
+// identical ylops take non-decreasing anchors, polys are tried by distinct shape).  Returns 1 (fits),
+// 0 (does not fit) or -1: the search passed kFitCap nodes without an answer (the env's audit
+// then reports SPARC_RULE_SEARCH_EXHAUSTED; the reference would keep searching)
 template <int W>
-__device__ __noinline__ bool exact_fit(const FitIn& in, const BB<W>& Rc, uint32_t pitch, int32_t* err) {
+__device__ __noinline__ int exact_fit(const FitIn& in, const BB<W>& Rc, uint32_t pitch) {
     const RulesTab& rt = *in.rt;
     const uint32_t CX = in.CX, CY = in.CY;
     FitGrid g;
@@ -189,7 +191,7 @@ __device__ __noinline__ bool exact_fit(const FitIn& in, const BB<W>& Rc, uint32_
     cur[0] = -1;
     uint32_t iters = 0;
     while (true) {
-        if (++iters > kFitCap) { atomicOr(err, (int)kErrRuleSearch); return false; }
+        if (++iters > kFitCap) return -1;
         if (L < ny) {                                            // _polyfit_place_ylops
             int a = cur[L];
             if (a >= 0) g.add(ypat[L] << a);
@@ -197,7 +199,7 @@ __device__ __noinline__ bool exact_fit(const FitIn& in, const BB<W>& Rc, uint32_
             const uint64_t cand = a < 64 ? yva[L] & (~0ull << a) : 0ull;
             if (!cand) {
                 cur[L] = -1;
-                if (L == 0) return false;
+                if (L == 0) return 0;
                 --L;
                 continue;
             }
@@ -217,8 +219,8 @@ __device__ __noinline__ bool exact_fit(const FitIn& in, const BB<W>& Rc, uint32_
             else if (L == LMAX) { done = true; ok = ng == 0; }    // no polys left
             else if (ng == 0) { done = true; ok = true; }        // no negative cell: True
             if (done) {
-                if (ok) return true;
-                if (L == 0) return false;
+                if (ok) return 1;
+                if (L == 0) return 0;
                 --L;
                 continue;
             }
@@ -231,7 +233,7 @@ __device__ __noinline__ bool exact_fit(const FitIn& in, const BB<W>& Rc, uint32_
         while (j < nd && (cnt[j] == 0 || !((dva[j] >> pat[lv]) & 1ull))) ++j;
         if (j >= nd) {
             cur[L] = -1;
-            if (L == 0) return false;
+            if (L == 0) return 0;
             --L;
             continue;
         }
@@ -272,7 +274,7 @@ __device__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const BB<W>& vi
     const uint32_t ir = rt.inst_range[q];
     const FitIn fin{&rt, ir & 0xFFFFu, ir >> 16, (X - 1) / 2, (Y - 1) / 2};
 
-    bool sq_ok = true, star_ok = true, poly_ok = true;
+    bool sq_ok = true, star_ok = true, poly_ok = true, exhausted = false;
     uint64_t fit_ok = 0;
     BB<W> remaining = cells;
     uint32_t rid = 0;
@@ -329,7 +331,11 @@ __device__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const BB<W>& vi
         }
         if (has) {
             bool ok = Rc.popc() == pa - ya;
-            if (ok) ok = exact_fit<W>(fin, Rc, P, p.err);
+            if (ok) {
+                const int r = exact_fit<W>(fin, Rc, P);
+                exhausted |= r < 0;
+                ok = r > 0;
+            }
             if (ok) fit_ok |= 1ull << (rid & 63);
             poly_ok &= ok;
         }
@@ -348,6 +354,7 @@ __device__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const BB<W>& vi
                     ((uint32_t)sq_ok << 4) | ((uint32_t)star_ok << 5) | ((uint32_t)tri_ok << 6) |
                     ((uint32_t)poly_ok << 7);
     bits |= (uint32_t)((bits & 0xFFu) == 0xFFu) << 8;
+    bits |= (uint32_t)exhausted << 9;
     return RuleOut<W>{bits, fit_ok};
 }
 

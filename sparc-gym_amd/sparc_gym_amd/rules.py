@@ -17,6 +17,7 @@ RULE_NAMES = ("reached_target", "path_not_crossing", "no_gap_violations", "all_d
               "square_color_separation", "star_pairing_exact", "triangles_edge_count", "poly_ylop_area",
               "all_rules_satisfied")
 SKIP_LAYERS = ("visited", "gaps", "agent_location", "target_location")
+RULE_SEARCH_EXHAUSTED = 1 << 9   # SPARC_RULE_SEARCH_EXHAUSTED: an exact-fit search hit its node cap
 
 
 def region_map_of(region_bits, x_size, y_size, pitch):
@@ -29,6 +30,11 @@ def region_map_of(region_bits, x_size, y_size, pitch):
 def rule_status(puzzle, obs_array, path, agent, target, bits, region_map, fit, terminated=False,
                 truncated=False):
     """The reference's rule_status dict (structure of SPaRC_Gym.py:896-950)."""
+    if int(bits) & RULE_SEARCH_EXHAUSTED:
+        # the kernel caps each exact-fit search (sparc_rules.hpp kFitCap); past it the poly/ylop
+        # answer is unknown, and a guessed dict would silently differ from the reference's
+        raise RuntimeError("rule audit: the poly/ylop exact-fit search of this state passed its node cap "
+                           "(SPARC_RULE_SEARCH_EXHAUSTED); poly_ylop_area cannot be reported")
     color = np.asarray(puzzle["color_array"])
     add = np.asarray(puzzle["additional_info"])
     passed = {n: bool((int(bits) >> k) & 1) for k, n in enumerate(RULE_NAMES)}

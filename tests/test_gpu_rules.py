@@ -82,17 +82,20 @@ def _state_points(vis_words, pitch, X, Y):
     return [[x, y] for x in range(X) for y in range(Y) if (v >> (x * pitch + y)) & 1]
 
 
-# random symbol soups only up to 11x11: on 13x13 / 15x15 boards they can hold regions with many
-# ylops, whose exact-fit search (anchors^ylops, as in the reference) is effectively unbounded
-@pytest.mark.parametrize("sizes,full,n", [(((3, 3),), True, 65536), (((2, 2), (3, 3), (4, 4), (5, 5)), True, 8192),
-                                          (((7, 7), (6, 6)), False, 4096)])
-def test_rules_at_scale_vs_oracle(on_gpu, sizes, full, n):
+# unbounded random symbol soups only up to 11x11: on 13x13 / 15x15 boards they can hold regions
+# with many ylops, whose exact-fit search (anchors^ylops, as in the reference) is effectively
+# unbounded; there the soup is capped at 4 poly / ylop cells per puzzle (max_shaped)
+@pytest.mark.parametrize("sizes,full,n,max_shaped", [(((3, 3),), True, 65536, None),
+                                                     (((2, 2), (3, 3), (4, 4), (5, 5)), True, 8192, None),
+                                                     (((7, 7), (6, 6)), False, 4096, None),
+                                                     (((7, 7), (6, 6)), True, 4096, 4)])
+def test_rules_at_scale_vs_oracle(on_gpu, sizes, full, n, max_shaped):
     """After a device rollout of random actions, k_rules bits equal the oracle's on a sample."""
     from sparc_gym_amd import SPaRCVecEnv, synthetic
     from sparc_gym_amd.puzzles import process_puzzles
     recs = synthetic.make_rule_puzzles(256, seed=8, sizes=sizes, break_prob=0.3)
     if full:
-        recs += synthetic.make_puzzles(256, seed=7, sizes=sizes, full_properties=True)
+        recs += synthetic.make_puzzles(256, seed=7, sizes=sizes, full_properties=True, max_shaped=max_shaped)
     proc = process_puzzles(recs)
     vec = SPaRCVecEnv(n, processed=proc, traceback=True, autoreset="next_step", observation="compact",
                       rules=True)
@@ -105,6 +108,7 @@ def test_rules_at_scale_vs_oracle(on_gpu, sizes, full, n):
         if T:
             vec.rollout(T, None, seed=T, record=False)
         bits = vec.rule_audit()["bits"].cpu().numpy().astype(np.uint16)
+        assert not (bits & (1 << 9)).any()   # no exact-fit search reached its node cap
         st = vec.state()
         for i in rng.choice(n, size=400, replace=False):
             q = int(st["puzzle"][i])

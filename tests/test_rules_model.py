@@ -82,3 +82,22 @@ def test_rule_status_layout_matches_reference(pool):
         got = rule_status(p, obs, s["path"], np.array(s["agent"]), np.array(p["target_location"]), bits,
                           region_map_of(reg, p["x_size"], p["y_size"], table.pitch), fit)
         assert rules_ref.normalize(got) == s["rule_status"], (pool, e, t)
+
+
+def test_exhausted_search_refuses_rule_status():
+    """An env whose exact-fit search hit the kernel's node cap (SPARC_RULE_SEARCH_EXHAUSTED) gets
+    no rule_status dict: its poly/ylop answer is unknown, so the host raises instead of guessing."""
+    import numpy as np
+    import pytest
+    from collections import OrderedDict
+    from sparc_gym_amd.rules import RULE_SEARCH_EXHAUSTED, region_map_of, rule_status
+    g = load("rules_7x7_tb1")
+    proc = process_puzzles(g["records"])
+    table = pack_table(proc)
+    p = proc[0]
+    obs = OrderedDict((k, v.copy()) for k, v in p["obs_array"].items())
+    reg = np.full(64 * table.words, 255, np.uint8)
+    with pytest.raises(RuntimeError, match="node cap"):
+        rule_status(p, obs, [list(p["start_location"])], np.array(p["start_location"]),
+                    np.array(p["target_location"]), RULE_SEARCH_EXHAUSTED,
+                    region_map_of(reg, p["x_size"], p["y_size"], table.pitch), 0)
