@@ -41,7 +41,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level par
 # (MI355X_MICROARCH.md, Wave scheduling), at the 2.4 GHz peak engine clock
 VALU_PEAK_WAVE_INSTS = 1024 * 2.4e9 / 2
 CSRC_FILES = ("sparc-gym_amd/csrc/sparc_kernels.hip", "sparc-gym_amd/csrc/sparc_env.hpp",
-              "sparc-gym_amd/csrc/sparc_rules.hpp", "include/sparc_gym_amd.h", "sparc-gym_amd/Makefile")
+              "sparc-gym_amd/csrc/sparc_rules.hpp", "sparc-gym_amd/csrc/sparc_trie.hpp", "include/sparc_gym_amd.h", "sparc-gym_amd/Makefile")
 
 CONFIGS = {
     # name: (grid sizes, full property set, traceback, 'new' observation planes every step)
@@ -49,8 +49,12 @@ CONFIGS = {
     "c3": (((3, 3),), True, True, False),
     # BASELINE configs[3]: 262,144 mixed 5x5-11x11 puzzles, observation='new' dict pack
     "c4": (((2, 2), (3, 3), (4, 4), (5, 5)), True, True, True),
+    # c4's pool without the observation planes (the step compute of the mixed pool alone)
+    "c4c": (((2, 2), (3, 3), (4, 4), (5, 5)), True, True, False),
+    # the other reading of "7x7": a 7x7 cell grid, i.e. a 15x15 lattice (SPaRC_Gym.py:243-248)
+    "c3g7": (((7, 7),), True, True, False),
 }
-DEFAULT_ENVS = {"c2": 4096, "c3": 65536, "c4": 262144}
+DEFAULT_ENVS = {"c2": 4096, "c3": 65536, "c4": 262144, "c4c": 262144, "c3g7": 65536}
 
 
 def parse():

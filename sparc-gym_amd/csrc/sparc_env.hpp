@@ -50,6 +50,9 @@ struct Table {
     const uint64_t* __restrict__ init;  // [P] padded W = 1 layout: blocked board at reset
     const uint4* __restrict__ row1;     // [P] padded W = 1 layout: compact puzzle row
     const uint4* __restrict__ trie1;    // [nodes] W = 1 layout: packed nodes (see Env<1>)
+    const uint2* __restrict__ trie8;    // [nodes] split-kernel trie records (sparc_trie.hpp)
+    const uint4* __restrict__ trow;     // [P] split-kernel trie rows (sparc_trie.hpp)
+    const uint4* __restrict__ mrow;     // [P] W = 1 split move wave: {row1.x, reset board lo, hi, 0}
     uint32_t num_puzzles;
 };
 
@@ -455,9 +458,6 @@ struct Env<1, TB, Stack> {
     // solutions, done, reset step
     uint32_t s_a = 0, s_fwd = 0, s_pop = 0, s_mv = 0, s_done = 0, s_rs = 0;
     uint4 rec;
-    // k_rollout1s trie wave: the next puzzle's index and row (take_hand_word_pf)
-    uint4 nx;
-    uint32_t npid = 0;
     // k_rollout1s move wave: the next puzzle's index, row word and reset board, loaded at the
     // previous reset (reset_next_pf)
     uint32_t rpid = 0, rrow = 0;
@@ -552,18 +552,18 @@ struct Env<1, TB, Stack> {
         }
     }
 
-    // reset_next with the next puzzle's row word and board already in registers: they were read
-    // from LDS at the previous reset (or at load), so a reset waits on no LDS read (MI355X, c3:
-    // 0.466 -> 0.460 ms per 2,000-step launch); a resetting lane then reads the rows of the
-    // puzzle after the new one, for its next reset
-    template <class Src>
-    __device__ __forceinline__ void prefetch_reset(const Src& src, uint32_t num_puzzles) {
+    // reset_next with the next puzzle's row word and board already in registers (k_rollout1s
+    // move wave): they were read at the previous reset (or at load), so a reset waits on no
+    // read (MI355X, c3: 0.466 -> 0.460 ms per 2,000-step launch); a resetting lane then reads
+    // the row of the puzzle after the new one, for its next reset.  Move rows (split kernel):
+    // {row1.x, reset board lo, hi, 0}.
+    __device__ __forceinline__ void prefetch_reset_m(const uint4* mrow, uint32_t num_puzzles) {
         rpid = pid + 1 == num_puzzles ? 0u : pid + 1;
-        rrow = src.get_row1(rpid).x;
-        rinit = src.get_init(rpid);
+        const uint4 m = mrow[rpid];
+        rrow = m.x;
+        rinit = ((uint64_t)m.z << 32) | m.y;
     }
-    template <class Src>
-    __device__ __forceinline__ void reset_next_pf(const Params& p, const Src& src) {
+    __device__ __forceinline__ void reset_next_m(const Params& p, const uint4* mrow) {
         if (pending & (uint32_t)(p.autoreset == 1)) {
             pid = rpid;
             e = rrow & 0xFFu;
@@ -574,10 +574,9 @@ struct Env<1, TB, Stack> {
             len = 1;
             step = -1;   // this step's increment brings it to 0
             rs = 1;
-            prefetch_reset(src, p.tab.num_puzzles);
+            prefetch_reset_m(mrow, p.tab.num_puzzles);
         }
     }
-
     __device__ __forceinline__ uint32_t phase_move(const Params& p, uint32_t a) {
         const uint32_t P = p.pitch;
         step = __builtin_elementwise_add_sat(step, 1);                              // 1132
@@ -621,19 +620,10 @@ struct Env<1, TB, Stack> {
         return f;
     }
 
-    // COND_GATHER: gather the record only for lanes whose node moved (exec-masked; most waves
-    // skip it).  The branch costs ~5% with one wave per SIMD, where the unconditional gather's
-    // latency is hidden anyway; with two waves per SIMD the gathers themselves are the limit
-    // (MI355X, c3: 2.24e11 -> 2.94e11 env-steps/s at 131,072 envs), so the split kernel uses it.
-    // ROOT_SET: the caller already put a reset step's trie state at the root (take_hand_word,
-    // inside its reset branch), so the per-step selects are skipped.
-    template <bool COND_GATHER = false, bool ROOT_SET = false>
     __device__ __forceinline__ int phase_trie(const Params& p) {
         // a reset step starts the new puzzle's trie at its root
-        if constexpr (!ROOT_SET) {
-            nn = pick(s_rs != 0u, ((pflags >> 3) & 1u) << 15, nn);
-            off = pick(s_rs != 0u, ((pflags >> 1) & 1u) ^ 1u, off);
-        }
+        nn = pick(s_rs != 0u, ((pflags >> 3) & 1u) << 15, nn);
+        off = pick(s_rs != 0u, ((pflags >> 1) & 1u) ^ 1u, off);
         // solution trie (first read of the record loaded at the previous step): a forward move
         // on the trie goes to the child (or leaves the trie), a pop on the trie to the parent,
         // off the trie they count the depth off it
@@ -645,7 +635,7 @@ struct Env<1, TB, Stack> {
         nn = pick(down, c, pick(up, rec.z, nn));
         off = pick(on, s_fwd & (uint32_t)!has, off + s_fwd - s_pop);
         // the record changes only with the node (a random walk is off the trie on most steps)
-        if (!COND_GATHER || (down | up | (s_rs != 0u))) load_rec(p);
+        load_rec(p);
         // reward code (1204-1223): done: +100 on a solution, else -100 unless the previous
         // done step already set outcome_reward = 1 (then 0); otherwise +-1 when moved (0 if the
         // puzzle has no solutions); a reset step returns 0 (no move, not done)
@@ -665,80 +655,6 @@ struct Env<1, TB, Stack> {
         flags = phase_move(p, a);
         was_reset = s_rs;
         return phase_trie(p);
-    }
-
-    // ---- k_rollout1s: the step split over a move wave (reset_next + phase_move) and a trie
-    // wave (phase_trie).  The move wave hands each step over as one 16-bit LDS word: its flag
-    // byte f (term | trunc << 1 | legal << 2 | reset << 6) | pop << 8 | forward << 9 | action
-    // << 10.  The trie wave derives done (f & 3), the reset step (bit 6) and
-    // moved-with-solutions (forward or pop, on a puzzle with solutions) from it, so the move
-    // wave's serial chain only packs three fields.  An action >= 4 never moves (forward = pop
-    // = 0); its bits above 15 are cut by the 16-bit store, and the trie wave reads only
-    // action & 3, which the cut keeps.  The I/O wave stores the low bytes as the flag output.
-    __device__ __forceinline__ uint32_t hand_word(uint32_t f) const {
-        return (((((s_a << 1) | s_fwd) << 1) | s_pop) << 8) | f;
-    }
-    // the trie wave's side: unpack the word; a reset step moves to the next puzzle's rows, as
-    // the move wave's reset_next did for its part (index + 1 mod P, SPaRC_Gym.py:1087), and
-    // to its trie root
-    template <class Src>
-    __device__ __forceinline__ void take_hand_word(const Src& src, uint32_t num_puzzles, uint32_t hw) {
-        s_rs = (hw >> 6) & 1u;
-        s_pop = TB ? (hw >> 8) & 1u : 0u;   // no pops without traceback
-        s_fwd = (hw >> 9) & 1u;
-        s_a = (hw >> 10) & 3u;
-        s_done = (uint32_t)((hw & 3u) != 0u);
-        if (s_rs) {   // the new puzzle's rows and its trie root (phase_trie<.., true>)
-            pid = pid + 1 == num_puzzles ? 0u : pid + 1;
-            (void)load_puzzle(src, pid);
-            nn = ((pflags >> 3) & 1u) << 15;
-            off = ((pflags >> 1) & 1u) ^ 1u;
-        }
-        s_mv = (s_fwd | s_pop) & pflags & 1u;
-    }
-    // ---- k_rollout1s trie wave without traceback: the next puzzle's row (the autoreset
-    // always loads pid + 1 mod P, SPaRC_Gym.py:1087) is read from LDS one step ahead, every
-    // step, into nx, so that a reset step applies registers instead of waiting on an LDS read
-    // (a 64-lane wave has a resetting lane on most steps).  npid = the puzzle after pid.
-    // MI355X, 2,000-step launches: c2 pool 0.453 -> 0.435 ms at 65,536 envs and 0.412 ->
-    // 0.398 ms at 4,096; with traceback (c3) 0.472 -> 0.478 ms, so TB keeps take_hand_word.
-    // The same prefetch in the move wave was slower for both.
-    __device__ __forceinline__ static uint32_t next_pid(uint32_t q, uint32_t num_puzzles) {
-        return q + 1 == num_puzzles ? 0u : q + 1;
-    }
-    template <class Src>
-    __device__ __forceinline__ void prefetch_trie(const Src& src) {
-        nx = src.get_row1(npid);
-    }
-    template <class Src>
-    __device__ __forceinline__ void take_hand_word_pf(const Src& src, uint32_t num_puzzles, uint32_t hw) {
-        s_rs = (hw >> 6) & 1u;
-        s_pop = TB ? (hw >> 8) & 1u : 0u;
-        s_fwd = (hw >> 9) & 1u;
-        s_a = (hw >> 10) & 3u;
-        s_done = (uint32_t)((hw & 3u) != 0u);
-        if (s_rs) {
-            pid = npid;
-            npid = next_pid(npid, num_puzzles);
-            (void)apply_row(nx);
-            nn = ((pflags >> 3) & 1u) << 15;
-            off = ((pflags >> 1) & 1u) ^ 1u;
-        }
-        prefetch_trie(src);
-        s_mv = (s_fwd | s_pop) & pflags & 1u;
-    }
-
-    // the trie wave's part of load(): puzzle rows, trie state and the node's record
-    template <class Src>
-    __device__ __forceinline__ void load_trie(const Params& p, const Src& src, uint32_t i) {
-        const State& s = p.st;
-        const uint32_t ps = s.pos[i], ax = s.aux[i];
-        off = ps >> 24;
-        nn = (ax & 0x7FFFu) | (((ax >> 19) & 1u) << 15);
-        outcome = (ax >> 16) & 3u;
-        pid = s.pid[i];
-        (void)load_puzzle(src, pid);
-        load_rec(p);
     }
 
     // the code and solved flag that phase_trie would report again for the last step of the

@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "sparc_env.hpp"
+#include "sparc_trie.hpp"
 #include "sparc_rules.hpp"
 #include "sparc_gym_amd.h"
 
@@ -590,26 +591,35 @@ __global__ void __launch_bounds__(kBlock1) k_rollout1(Params p, int32_t T, const
 // A lone wave issues one instruction every ~5 cycles while its SIMD can take one every ~2.5
 // from two waves, and at 65,536 envs there is exactly one 64-env wave per SIMD.  So the step is
 // cut where its data flow is one-way: a MOVE wave runs the autoreset, legality, move, path and
-// flags (reset_next + phase_move) and hands each env-step's flag byte and trie inputs to a TRIE
-// wave as one 16-bit LDS word (hand_word); the trie wave runs the solution-trie transition,
-// the record gather and the reward code (phase_trie) one 16-step tile behind.  Nothing flows
-// back: the reward code never feeds the move.  I/O waves stream action tiles in and reward /
-// flag tiles out as in k_rollout1.  Per workgroup 256 envs = 4 move waves (0-3) + 4 trie waves
-// (4-7, on the same SIMDs as the move waves of their envs) + 4 I/O waves (8-11, one per SIMD);
-// one barrier per tile:
+// flags (reset_next + phase_move) and hands each env-step over to a TRIE wave as one 32-bit LDS
+// word (hand_word32, sparc_trie.hpp); the trie wave (TrieLane) runs the solution-trie walk, the
+// record gathers, the reward code and the episode counters one 16-step tile behind.  Nothing
+// flows back: the reward code never feeds the move.  I/O waves stream action tiles in and
+// reward / flag tiles out.  Per workgroup 256 envs = 4 move waves (0-3) + 4 trie waves (4-7, on
+// the same SIMDs as the move waves of their envs) + 4 I/O waves (8-11, one per SIMD); one
+// barrier per tile:
 //   interval k (between barriers B_k and B_k+1): move waves step tile k; trie waves finish
 //   tile k-1; the I/O waves load the actions of tile k+1 and store the outputs of tile k-2.
 // Only full workgroups, T % 16 == 0 and 16-B aligned I/O; the host runs any tail through
 // k_rollout1.  The state after the launch is the same SoA record (the trie wave hands its
-// final node / depth / outcome and stats to the move wave through LDS before the store).
+// final trie state and counters to the move wave through LDS before the store).
 constexpr int kBlock1s = 768;
 constexpr size_t kS_Act = 0;                          // actions [2 tiles][16][64]
 constexpr size_t kS_Rew = kS_Act + 2 * kTile * 64;    // reward ring [64 steps][64]
-constexpr size_t kS_FH = kS_Rew + kRing * 64;         // flag | hand-over ring [64 steps][64] u16
-constexpr size_t kS_Stk = kS_FH + 2 * kRing * 64;     // move stack [64 moves][64]
+constexpr size_t kS_FH = kS_Rew + kRing * 64;         // hand-over ring [64 steps][64] u32
+constexpr size_t kS_Stk = kS_FH + 4 * kRing * 64;     // move stack [64 moves][64]
 constexpr size_t kS_Pair = kS_Stk + 64 * 64;          // per move / trie wave pair
 constexpr size_t kS_Fin = 4 * kS_Pair;                // trie wave's final state [4][64] 2 x uint4
 constexpr size_t kS_Base = kS_Fin + 4 * 64 * 2 * sizeof(uint4);
+// LDS bytes of the staged rows: move rows + trie rows, 16 B each per puzzle
+__host__ __device__ constexpr size_t split_table_bytes(uint32_t P) { return (size_t)P * 2 * sizeof(uint4); }
+
+// the flag bytes (byte 1) of four hand-over words
+__device__ __forceinline__ uint32_t flag_bytes4(const u32x4 w) {
+    const uint32_t lo = __builtin_amdgcn_perm(w.y, w.x, 0x0C0C0501u);
+    const uint32_t hi = __builtin_amdgcn_perm(w.w, w.z, 0x0C0C0501u);
+    return lo | (hi << 16);
+}
 
 template <bool TB, bool RAND, bool LDS_TABLE>
 __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, const uint8_t* __restrict__ act,
@@ -617,17 +627,19 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
                                                         uint8_t* __restrict__ flg, int4* __restrict__ stats) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    PuzzleSrc<1> src{p.tab.info, p.tab.root, p.tab.open, p.tab.init, p.tab.row1};
+    const uint32_t NP = p.tab.num_puzzles;
+    const uint4* mrow = p.tab.mrow;
+    const uint4* trow = p.tab.trow;
     if constexpr (LDS_TABLE) {
-        const uint32_t P = p.tab.num_puzzles;
-        uint4* lrow1 = reinterpret_cast<uint4*>(smem + kS_Base);
-        uint64_t* linit = reinterpret_cast<uint64_t*>(lrow1 + P);
-        for (uint32_t k = threadIdx.x; k < P; k += kBlock1s) {
-            lrow1[k] = p.tab.row1[k];
-            linit[k] = p.tab.init[k];
+        uint4* lm = reinterpret_cast<uint4*>(smem + kS_Base);
+        uint4* lt = lm + NP;
+        for (uint32_t k = threadIdx.x; k < NP; k += kBlock1s) {
+            lm[k] = p.tab.mrow[k];
+            lt[k] = p.tab.trow[k];
         }
         __syncthreads();
-        src = PuzzleSrc<1>{p.tab.info, p.tab.root, p.tab.open, linit, lrow1};
+        mrow = lm;
+        trow = lt;
     }
     const size_t n = p.n;
     const uint32_t wg_base = blockIdx.x * 256u;
@@ -648,26 +660,20 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         };
         auto store_tile = [&](int32_t k) {                       // whole 128-B lines, as k_rollout1
             const uint32_t r8 = lane >> 3, c8 = (lane & 7u) * 16u;
-            {
-                const uint32_t h = io >> 1, q = io & 1u;
-                const uint32_t row = (uint32_t)((k * kTile) & (kRing - 1)) + h * 8 + r8;
-                {
-                    const uint32_t w = 2 * q + (c8 >> 6);
-                    const uint8_t* base = smem + w * kS_Pair + row * 64 + (c8 & 63u);
-                    const size_t o = (size_t)(k * kTile + h * 8 + r8) * n + wg_base + q * 128 + c8;
-                    if (rew) nt_store16(reinterpret_cast<uint8_t*>(rew) + o, *reinterpret_cast<const u32x4*>(base + kS_Rew));
-                    if (flg) {   // the low bytes of 16 u16 ring entries (flag | hand-over << 8)
-                        const uint8_t* fh = smem + w * kS_Pair + kS_FH + row * 128 + 2 * (c8 & 63u);
-                        const u32x4 a = *reinterpret_cast<const u32x4*>(fh);
-                        const u32x4 b = *reinterpret_cast<const u32x4*>(fh + 16);
-                        u32x4 v;
-                        v.x = __builtin_amdgcn_perm(a.y, a.x, 0x06040200u);
-                        v.y = __builtin_amdgcn_perm(a.w, a.z, 0x06040200u);
-                        v.z = __builtin_amdgcn_perm(b.y, b.x, 0x06040200u);
-                        v.w = __builtin_amdgcn_perm(b.w, b.z, 0x06040200u);
-                        nt_store16(flg + o, v);
-                    }
-                }
+            const uint32_t h = io >> 1, q = io & 1u;
+            const uint32_t row = (uint32_t)((k * kTile) & (kRing - 1)) + h * 8 + r8;
+            const uint32_t w = 2 * q + (c8 >> 6);
+            const uint8_t* base = smem + w * kS_Pair + row * 64 + (c8 & 63u);
+            const size_t o = (size_t)(k * kTile + h * 8 + r8) * n + wg_base + q * 128 + c8;
+            if (rew) nt_store16(reinterpret_cast<uint8_t*>(rew) + o, *reinterpret_cast<const u32x4*>(base + kS_Rew));
+            if (flg) {   // byte 1 of 16 hand-over words
+                const u32x4* fh = reinterpret_cast<const u32x4*>(smem + w * kS_Pair + kS_FH + row * 256 + 4 * (c8 & 63u));
+                u32x4 v;
+                v.x = flag_bytes4(fh[0]);
+                v.y = flag_bytes4(fh[1]);
+                v.z = flag_bytes4(fh[2]);
+                v.w = flag_bytes4(fh[3]);
+                nt_store16(flg + o, v);
             }
         };
         if (K > 0) load_tile(0);
@@ -686,17 +692,15 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
     const uint32_t i = wg_base + pr * 64u + lane;
     uint8_t* pb = smem + pr * kS_Pair;
     uint4* fin = reinterpret_cast<uint4*>(smem + kS_Fin) + 2u * (pr * 64u + lane);
-    using Stack = typename std::conditional<TB, LdsStack<64>, RegStack>::type;
-    Env<1, TB, Stack> e;
     if (wv < 4) {                                                // ---- move waves
+        const PuzzleSrc<1> src{p.tab.info, p.tab.root, p.tab.open, p.tab.init, p.tab.row1};
+        Env<1, TB, typename std::conditional<TB, LdsStack<64>, RegStack>::type> e;
         if constexpr (TB) e.stk.col = pb + kS_Stk + lane;
         e.load(p, src, i);
-        e.prefetch_reset(src, p.tab.num_puzzles);
+        e.prefetch_reset_m(mrow, NP);
+        const uint32_t pend0 = e.pending;
         const uint64_t gid = p.env_offset + i;
-        uint16_t* tf = reinterpret_cast<uint16_t*>(pb + kS_FH) + lane;
-        // done / reset counts: with traceback the move wave is the longer chain and the trie
-        // wave counts them (from the hand-over word); without, the move wave counts them
-        uint32_t acc_y = 0, acc_w = 0;
+        uint32_t* th = reinterpret_cast<uint32_t*>(pb + kS_FH) + lane;
         __syncthreads();                                         // B_0
         for (int32_t k = 0; k < K; ++k) {
             const uint8_t* ta = pb + kS_Act + (k & 1) * (kTile * 64) + lane;
@@ -709,13 +713,9 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const uint32_t row = (uint32_t)(k * kTile + g + j) & (kRing - 1);
-                    e.reset_next_pf(p, src);
+                    e.reset_next_m(p, mrow);
                     const uint32_t f = e.phase_move(p, av[j]);
-                    tf[row * 64] = (uint16_t)e.hand_word(f);
-                    if constexpr (!TB) {
-                        acc_y += e.pending;
-                        acc_w += e.s_rs;
-                    }
+                    th[row * 64] = hand_word32(e.s_a, e.s_fwd, e.s_pop, f, e.s_done, e.s_mv);
                 }
             }
             __syncthreads();                                     // B_{k+1}
@@ -723,17 +723,19 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         __syncthreads();                                         // B_{K+1}
         __syncthreads();                                         // B_{K+2}: the trie state is in fin
         const uint4 fs = fin[0];
+        const uint4 fc = fin[1];
         e.nn = fs.x & 0xFFFFu;
-        e.outcome = fs.x >> 16;
-        e.off = fs.y;
+        e.off = fs.x >> 16;
+        e.outcome = e.pending ? (fs.y == 0u ? 1u : 2u) : 0u;   // outcome_reward after the last step
         e.store(p, src, i);
         if (stats) {
-            const uint4 fc = fin[1];
+            // autoresets: one per done step before the last, plus one for a done step carried in
+            const uint32_t resets = p.autoreset == 1 ? pend0 + fc.x - e.pending : 0u;
             int4 st = stats[i];
             st.x += (int)fs.z;
-            st.y += (int)(fc.x + acc_y);
+            st.y += (int)fc.x;
             st.z += (int)fs.w;
-            st.w += (int)(fc.y + acc_w);
+            st.w += (int)resets;
             stats[i] = st;
         }
     } else {                                                     // ---- trie waves
@@ -741,43 +743,27 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         // carries the record-gather waits, the move wave has slack (c3: 0.289 -> 0.266 ms per
         // 1,000 steps; priority to the move wave instead: no change)
         __builtin_amdgcn_s_setprio(1);
-        e.load_trie(p, src, i);
-        if constexpr (!TB) {
-            e.npid = e.next_pid(e.pid, p.tab.num_puzzles);
-            e.prefetch_trie(src);
-        }
-        const uint16_t* th = reinterpret_cast<const uint16_t*>(pb + kS_FH) + lane;
+        TrieLane tl;
+        tl.load(p.st.pos[i], p.st.aux[i], p.st.pid[i], trow, p.tab.trie8, NP);
+        const uint32_t* th = reinterpret_cast<const uint32_t*>(pb + kS_FH) + lane;
         uint8_t* tr = pb + kS_Rew + lane;
-        int acc_x = 0;
-        uint32_t acc_z = 0, acc_y = 0, acc_w = 0;
         __syncthreads();                                         // B_0
         __syncthreads();                                         // B_1 (interval 0: no tile yet)
         for (int32_t k = 1; k <= K; ++k) {
 #pragma unroll 1
             for (int g = 0; g < kTile; g += 4) {
-                // the group's 4 flag | hand-over words first (one LDS wait), then its 4 steps
+                // the group's 4 hand-over words first (one LDS wait), then its 4 steps
                 const uint32_t row0 = (uint32_t)((k - 1) * kTile + g) & (kRing - 1);
                 uint32_t hb[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) hb[j] = th[(row0 + j) * 64];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    if constexpr (TB) e.take_hand_word(src, p.tab.num_puzzles, hb[j]);
-                    else e.take_hand_word_pf(src, p.tab.num_puzzles, hb[j]);
-                    const int code = e.template phase_trie<true, true>(p);
-                    tr[(row0 + j) * 64] = (uint8_t)code;
-                    acc_x += code;
-                    acc_z += e.solved;
-                    if constexpr (TB) {
-                        acc_y += e.s_done;
-                        acc_w += e.s_rs;
-                    }
-                }
+                for (int j = 0; j < 4; ++j) tr[(row0 + j) * 64] = (uint8_t)tl.step(hb[j], trow, p.tab.trie8, NP);
             }
             __syncthreads();                                     // B_{k+1}
         }
-        fin[0] = make_uint4(e.nn | (e.outcome << 16), e.off, (uint32_t)acc_x, acc_z);
-        fin[1] = make_uint4(acc_y, acc_w, 0u, 0u);
+        fin[0] = make_uint4(tl.S, (uint32_t)tl.Oneg, (uint32_t)tl.acc_x, tl.acc_z);
+        fin[1] = make_uint4(tl.acc_y, 0u, 0u, 0u);
         __syncthreads();                                         // B_{K+2}
     }
 }
@@ -838,6 +824,8 @@ struct Ctx {
     uint4 *t_info = nullptr, *t_root = nullptr, *t_trie = nullptr, *t_trie1 = nullptr;
     uint64_t* t_init = nullptr;
     uint4* t_row1 = nullptr;
+    uint2* t_trie8 = nullptr;          // split-kernel tables (null: a puzzle's trie exceeds 15-bit nodes)
+    uint4 *t_trow = nullptr, *t_mrow = nullptr;
     int32_t* err = nullptr;
     uint8_t *s_act = nullptr, *s_flags = nullptr, *s_mask = nullptr;
     int8_t* s_rew = nullptr;
@@ -894,6 +882,9 @@ Params make_params(const Ctx* c) {
     p.tab.trie1 = c->t_trie1;
     p.tab.init = c->t_init;
     p.tab.row1 = c->t_row1;
+    p.tab.trie8 = c->t_trie8;
+    p.tab.trow = c->t_trow;
+    p.tab.mrow = c->t_mrow;
     p.tab.num_puzzles = c->num_puzzles;
     p.st.vis = c->vis;
     p.st.dirs = c->dirs;
@@ -1014,7 +1005,7 @@ int sparc_destroy(void* ctx) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->vis, c->dirs, c->pos, c->aux, c->step, c->pid, c->t_open, c->t_info, c->t_root, c->t_trie, c->t_trie1, c->t_init, c->t_row1,
-                    c->err, c->s_act, c->s_flags, c->s_mask, c->s_rew, c->s_pidx, c->r_planes, c->r_inst_range,
+                    c->t_trie8, c->t_trow, c->t_mrow, c->err, c->s_act, c->s_flags, c->s_mask, c->s_rew, c->s_pidx, c->r_planes, c->r_inst_range,
                     c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off, c->s_bits, c->s_region, c->s_fit};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -1108,6 +1099,12 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
     if (c->t_root) HIPCHK(c, hipFree(c->t_root));
     if (c->t_init) HIPCHK(c, hipFree(c->t_init));
     if (c->t_row1) HIPCHK(c, hipFree(c->t_row1));
+    if (c->t_trie8) HIPCHK(c, hipFree(c->t_trie8));
+    if (c->t_trow) HIPCHK(c, hipFree(c->t_trow));
+    if (c->t_mrow) HIPCHK(c, hipFree(c->t_mrow));
+    c->t_trie8 = nullptr;
+    c->t_trow = nullptr;
+    c->t_mrow = nullptr;
     c->t_init = nullptr;
     c->t_row1 = nullptr;
     c->t_open = nullptr;
@@ -1184,6 +1181,61 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
         }
         HIPCHK(c, hipMalloc(&c->t_trie1, sizeof(uint4) * nn));
         HIPCHK(c, hipMemcpy(c->t_trie1, t1.data(), sizeof(uint4) * nn, hipMemcpyHostToDevice));
+    }
+    // split-kernel tables (sparc_trie.hpp): 8-B records, field d = the child in direction d,
+    // and the parent in the field of the direction back to it (the reverse of the move that
+    // reached the node: no reachable child lives there, as that point is on the path); per
+    // puzzle the trie row (root children, base, max node, flags) and, for W = 1, the move row
+    bool small = true;
+    for (size_t q = 0; q < P; ++q)
+        if (((t->info[4 * q + 1] >> 16) & 2u) && (t->info[4 * q + 3] & 0xFFFFu) > 0x7FFFu) small = false;
+    if (small) {
+        std::vector<uint2> t8(nn, make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu));
+        auto packed = [&](size_t base, uint32_t k) {   // node k of a puzzle as index | terminal << 15
+            return k | (((t->trie[4 * (base + k) + 2] >> 16) & 1u) << 15);
+        };
+        for (size_t q = 0; q < P; ++q) {
+            const uint32_t* inf = t->info + 4 * q;
+            if (!((inf[1] >> 16) & 2u)) continue;
+            const size_t base = inf[2];
+            const uint32_t cnt = inf[3] & 0xFFFFu;
+            for (uint32_t k = 0; k < cnt; ++k) {
+                const uint32_t* r = t->trie + 4 * (base + k);
+                const uint32_t ch[4] = {r[0] & 0xFFFFu, r[0] >> 16, r[1] & 0xFFFFu, r[1] >> 16};
+                uint32_t f[4];
+                for (int d = 0; d < 4; ++d) f[d] = ch[d] == kNone ? 0xFFFFu : packed(base, ch[d]);
+                t8[base + k] = make_uint2(f[0] | (f[1] << 16), f[2] | (f[3] << 16));
+            }
+            for (uint32_t k = 0; k < cnt; ++k) {           // parents, after every child field
+                const uint32_t* r = t->trie + 4 * (base + k);
+                const uint32_t ch[4] = {r[0] & 0xFFFFu, r[0] >> 16, r[1] & 0xFFFFu, r[1] >> 16};
+                for (uint32_t d = 0; d < 4; ++d) {
+                    if (ch[d] == kNone) continue;
+                    uint2& cr = t8[base + ch[d]];
+                    const uint32_t back = d ^ 2u, sh = (back & 1u) * 16u;
+                    uint32_t& w = back < 2 ? cr.x : cr.y;
+                    w = (w & ~(0xFFFFu << sh)) | (packed(base, k) << sh);
+                }
+            }
+        }
+        std::vector<uint4> trow(P), mrow(P, make_uint4(0u, 0u, 0u, 0u));
+        for (size_t q = 0; q < P; ++q) {
+            const uint32_t* inf = t->info + 4 * q;
+            const uint32_t fl = (dinfo[q].y >> 16) & 0xFFFFu;
+            const uint32_t cnt = inf[3] & 0xFFFFu;
+            const uint2 rr = (fl & 2u) ? t8[inf[2]] : make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+            // flags as row1: bit0 solutions, bit1 root valid, bit3 root terminal
+            const uint32_t tf = (fl & 3u) | (((dinfo[q].y >> 19) & 1u) << 3);
+            const uint32_t rootS = (tf & 2u) ? ((tf >> 3) & 1u) << 15 : 0x10000u;
+            trow[q] = make_uint4(rr.x, rr.y, inf[2], rootS | ((cnt ? cnt - 1u : 0u) << 17));
+            if (W == 1) mrow[q] = make_uint4(row1[q].x, (uint32_t)init[q], (uint32_t)(init[q] >> 32), 0u);
+        }
+        HIPCHK(c, hipMalloc(&c->t_trie8, sizeof(uint2) * nn));
+        HIPCHK(c, hipMemcpy(c->t_trie8, t8.data(), sizeof(uint2) * nn, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMalloc(&c->t_trow, sizeof(uint4) * P));
+        HIPCHK(c, hipMemcpy(c->t_trow, trow.data(), sizeof(uint4) * P, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMalloc(&c->t_mrow, sizeof(uint4) * P));
+        HIPCHK(c, hipMemcpy(c->t_mrow, mrow.data(), sizeof(uint4) * P, hipMemcpyHostToDevice));
     }
     c->num_puzzles = (uint32_t)t->num_puzzles;
     c->num_nodes = (uint32_t)t->num_nodes;
@@ -1284,10 +1336,11 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
         // the full tiles of full workgroups go through the split move / trie kernel (MI355X, c3
         // at 65,536 envs: 0.266 vs 0.312 ms per 1,000 steps); a tail of T % 16 steps or a batch
         // that is not a multiple of 256 envs goes through k_rollout1 below
-        if (tiled && c->n % 256 == 0 && T >= kTile) {
+        if (tiled && c->n % 256 == 0 && T >= kTile && c->t_trie8) {
             const int32_t T16 = T / kTile * kTile;
-            const bool lds_s = kS_Base + tbytes <= budget;
-            const size_t shm_s = kS_Base + (lds_s ? tbytes : 0);
+            const size_t sbytes = split_table_bytes(c->num_puzzles);
+            const bool lds_s = kS_Base + sbytes <= budget;
+            const size_t shm_s = kS_Base + (lds_s ? sbytes : 0);
             auto launch_s = [&](auto kern, const uint8_t* a) {
                 if (shm_s > 64 * 1024 && (lds_rc = allow_big_lds(c, reinterpret_cast<const void*>(kern)))) return;
                 kern<<<dim3((unsigned)blocks), kBlock1s, shm_s, c->stream>>>(p, T16, a, seed, t0, d_rew, d_flags, st);
