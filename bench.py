@@ -321,6 +321,8 @@ def main():
     elif table.words == 1 and not obs:
         # batches of whole 256-env workgroups: the split move / trie kernel
         kernel = "k_rollout1s" if n % 256 == 0 and chunk >= 16 else "k_rollout1"
+    elif not obs and n % 256 == 0 and chunk >= 16:
+        kernel = "k_rolloutWs"   # the multi-word split kernel (when the pool fits its LDS layout)
     else:
         kernel = "k_rollout"
     workload = f"{args.config}_{args.mode}_n{n}_chunk{chunk if args.mode == 'rollout' else 1}"

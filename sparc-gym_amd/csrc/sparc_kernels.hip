@@ -22,6 +22,7 @@
 
 #include "sparc_env.hpp"
 #include "sparc_trie.hpp"
+#include "sparc_movew.hpp"
 #include "sparc_rules.hpp"
 #include "sparc_gym_amd.h"
 
@@ -768,6 +769,150 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Multi-word split rollout (k_rolloutWs, W = 2 / 4: lattices of 9x9 to 15x15 points).  The same
+// wave roles and tile schedule as k_rollout1s: per workgroup 256 envs = 4 move waves
+// (MoveLaneW, sparc_movew.hpp: the free board in LDS) + 4 trie waves (TrieLane, the same as
+// W = 1) + 4 I/O waves; 16-bit hand-over words.  LDS per pair (SplitGeom, runtime):
+//   actions [2][16][64] B | reward ring [64][64] B | hand-over ring [64][64] u16 |
+//   boards [BS][64] u32 | move stacks [M][64] B
+// then the trie waves' final state [4][64] 2 x uint4 and, when it fits, the trie rows.
+constexpr size_t kW_Act = 0, kW_Rew = 2 * kTile * 64, kW_Hand = kW_Rew + kRing * 64, kW_Board = kW_Hand + 2 * kRing * 64;
+__host__ __device__ constexpr size_t splitw_fin_bytes() { return 4 * 64 * 2 * sizeof(uint4); }
+
+template <int W, bool TB, bool RAND, bool LDS_TABLE>
+__global__ void __launch_bounds__(kBlock1s) k_rolloutWs(Params p, SplitGeom g, const uint4* __restrict__ mrow,
+                                                        const uint32_t* __restrict__ boards, int32_t T,
+                                                        const uint8_t* __restrict__ act, uint64_t seed, uint64_t t0,
+                                                        int8_t* __restrict__ rew, uint8_t* __restrict__ flg,
+                                                        int4* __restrict__ stats) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t NP = p.tab.num_puzzles;
+    const size_t fin_off = 4 * (size_t)g.pair;
+    const uint4* trow = p.tab.trow;
+    if constexpr (LDS_TABLE) {
+        uint4* lt = reinterpret_cast<uint4*>(smem + fin_off + splitw_fin_bytes());
+        for (uint32_t k = threadIdx.x; k < NP; k += kBlock1s) lt[k] = p.tab.trow[k];
+        __syncthreads();
+        trow = lt;
+    }
+    const size_t n = p.n;
+    const uint32_t wg_base = blockIdx.x * 256u;
+    const int32_t K = T / kTile;
+
+    if (wv >= 8) {                                               // ---- the I/O waves (as k_rollout1s)
+        const uint32_t io = wv - 8u;
+        const uint32_t r = lane >> 2, c = (lane & 3u) * 16u;
+        auto load_tile = [&](int32_t k) {
+            if constexpr (!RAND) {
+                const u32x4 v = nt_load16(act + (size_t)(k * kTile + r) * n + wg_base + io * 64 + c);
+                *reinterpret_cast<u32x4*>(smem + io * g.pair + kW_Act + (k & 1) * (kTile * 64) + r * 64 + c) = v;
+            }
+        };
+        auto store_tile = [&](int32_t k) {
+            const uint32_t r8 = lane >> 3, c8 = (lane & 7u) * 16u;
+            const uint32_t h = io >> 1, q = io & 1u;
+            const uint32_t row = (uint32_t)((k * kTile) & (kRing - 1)) + h * 8 + r8;
+            const uint32_t w = 2 * q + (c8 >> 6);
+            const uint8_t* base = smem + w * g.pair + row * 64 + (c8 & 63u);
+            const size_t o = (size_t)(k * kTile + h * 8 + r8) * n + wg_base + q * 128 + c8;
+            if (rew) nt_store16(reinterpret_cast<uint8_t*>(rew) + o, *reinterpret_cast<const u32x4*>(base + kW_Rew));
+            if (flg) {   // byte 1 of 16 u16 hand-over words
+                const u32x4* fh = reinterpret_cast<const u32x4*>(smem + w * g.pair + kW_Hand + row * 128 + 2 * (c8 & 63u));
+                const u32x4 a = fh[0], b = fh[1];
+                u32x4 v;
+                v.x = __builtin_amdgcn_perm(a.y, a.x, 0x07050301u);
+                v.y = __builtin_amdgcn_perm(a.w, a.z, 0x07050301u);
+                v.z = __builtin_amdgcn_perm(b.y, b.x, 0x07050301u);
+                v.w = __builtin_amdgcn_perm(b.w, b.z, 0x07050301u);
+                nt_store16(flg + o, v);
+            }
+        };
+        if (K > 0) load_tile(0);
+        __syncthreads();                                         // B_0
+        for (int32_t k = 0; k <= K; ++k) {
+            if (k + 1 < K) load_tile(k + 1);
+            if (k >= 2) store_tile(k - 2);
+            __syncthreads();                                     // B_{k+1}
+        }
+        if (K >= 1) store_tile(K - 1);
+        __syncthreads();                                         // B_{K+2}
+        return;
+    }
+
+    const uint32_t pr = wv & 3u;
+    const uint32_t i = wg_base + pr * 64u + lane;
+    uint8_t* pb = smem + pr * g.pair;
+    uint4* fin = reinterpret_cast<uint4*>(smem + fin_off) + 2u * (pr * 64u + lane);
+    if (wv < 4) {                                                // ---- move waves
+        MoveLaneW<TB> m;
+        m.bd = reinterpret_cast<uint32_t*>(pb + g.off_board) + lane;
+        m.col = pb + g.off_stack + lane;
+        m.template load<W>(p, g, mrow, i);
+        const uint32_t pend0 = m.pending;
+        const uint64_t gid = p.env_offset + i;
+        uint16_t* th = reinterpret_cast<uint16_t*>(pb + kW_Hand) + lane;
+        __syncthreads();                                         // B_0
+        for (int32_t k = 0; k < K; ++k) {
+            const uint8_t* ta = pb + kW_Act + (k & 1) * (kTile * 64) + lane;
+#pragma unroll 1
+            for (int gq = 0; gq < kTile; gq += 4) {
+                uint32_t av[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    av[j] = RAND ? uint_rand_action(seed, gid, t0 + (uint64_t)(k * kTile + gq + j)) : ta[(gq + j) * 64];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t row = (uint32_t)(k * kTile + gq + j) & (kRing - 1);
+                    m.reset_next(p, g, mrow, boards);
+                    const uint32_t f = m.phase_move(p, g, av[j]);
+                    th[row * 64] = (uint16_t)hand_word16(m.s_a, m.s_fwd, m.s_pop, f, m.s_done, m.s_mv);
+                }
+            }
+            __syncthreads();                                     // B_{k+1}
+        }
+        __syncthreads();                                         // B_{K+1}
+        __syncthreads();                                         // B_{K+2}: the trie state is in fin
+        const uint4 fs = fin[0];
+        const uint4 fc = fin[1];
+        m.template store<W>(p, g, i, fs.x, m.pending ? (fs.y == 0u ? 1u : 2u) : 0u);
+        if (stats) {
+            const uint32_t resets = p.autoreset == 1 ? pend0 + fc.x - m.pending : 0u;
+            int4 st = stats[i];
+            st.x += (int)fs.z;
+            st.y += (int)fc.x;
+            st.z += (int)fs.w;
+            st.w += (int)resets;
+            stats[i] = st;
+        }
+    } else {                                                     // ---- trie waves
+        __builtin_amdgcn_s_setprio(1);
+        TrieLane tl;
+        tl.load(p.st.pos[i], p.st.aux[i], p.st.pid[i], trow, p.tab.trie8, NP);
+        const uint16_t* th = reinterpret_cast<const uint16_t*>(pb + kW_Hand) + lane;
+        uint8_t* tr = pb + kW_Rew + lane;
+        __syncthreads();                                         // B_0
+        __syncthreads();                                         // B_1
+        for (int32_t k = 1; k <= K; ++k) {
+#pragma unroll 1
+            for (int gq = 0; gq < kTile; gq += 4) {
+                const uint32_t row0 = (uint32_t)((k - 1) * kTile + gq) & (kRing - 1);
+                uint32_t hb[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) hb[j] = th[(row0 + j) * 64];
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    tr[(row0 + j) * 64] = (uint8_t)tl.step(widen_hand_word(hb[j]), trow, p.tab.trie8, NP);
+            }
+            __syncthreads();                                     // B_{k+1}
+        }
+        fin[0] = make_uint4(tl.S, (uint32_t)tl.Oneg, (uint32_t)tl.acc_x, tl.acc_z);
+        fin[1] = make_uint4(tl.acc_y, 0u, 0u, 0u);
+        __syncthreads();                                         // B_{K+2}
+    }
+}
+
 template <int W>
 __global__ void __launch_bounds__(kBlock) k_obs_pack(Params p, int32_t* __restrict__ vis_out,
                                                      int32_t* __restrict__ agent_out, uint32_t xd, uint32_t yd) {
@@ -826,6 +971,12 @@ struct Ctx {
     uint4* t_row1 = nullptr;
     uint2* t_trie8 = nullptr;          // split-kernel tables (null: a puzzle's trie exceeds 15-bit nodes)
     uint4 *t_trow = nullptr, *t_mrow = nullptr;
+    // multi-word split kernel (k_rolloutWs): move rows and reset boards; split_w false when the
+    // pool does not fit its layout (pitch > 15, LDS, or no trie8)
+    uint4* t_mroww = nullptr;
+    uint32_t* t_boardw = nullptr;
+    SplitGeom sgeom{};
+    bool split_w = false;
     int32_t* err = nullptr;
     uint8_t *s_act = nullptr, *s_flags = nullptr, *s_mask = nullptr;
     int8_t* s_rew = nullptr;
@@ -1005,7 +1156,7 @@ int sparc_destroy(void* ctx) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->vis, c->dirs, c->pos, c->aux, c->step, c->pid, c->t_open, c->t_info, c->t_root, c->t_trie, c->t_trie1, c->t_init, c->t_row1,
-                    c->t_trie8, c->t_trow, c->t_mrow, c->err, c->s_act, c->s_flags, c->s_mask, c->s_rew, c->s_pidx, c->r_planes, c->r_inst_range,
+                    c->t_trie8, c->t_trow, c->t_mrow, c->t_mroww, c->t_boardw, c->err, c->s_act, c->s_flags, c->s_mask, c->s_rew, c->s_pidx, c->r_planes, c->r_inst_range,
                     c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off, c->s_bits, c->s_region, c->s_fit};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -1102,6 +1253,11 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
     if (c->t_trie8) HIPCHK(c, hipFree(c->t_trie8));
     if (c->t_trow) HIPCHK(c, hipFree(c->t_trow));
     if (c->t_mrow) HIPCHK(c, hipFree(c->t_mrow));
+    if (c->t_mroww) HIPCHK(c, hipFree(c->t_mroww));
+    if (c->t_boardw) HIPCHK(c, hipFree(c->t_boardw));
+    c->t_mroww = nullptr;
+    c->t_boardw = nullptr;
+    c->split_w = false;
     c->t_trie8 = nullptr;
     c->t_trow = nullptr;
     c->t_mrow = nullptr;
@@ -1236,6 +1392,49 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
         HIPCHK(c, hipMemcpy(c->t_trow, trow.data(), sizeof(uint4) * P, hipMemcpyHostToDevice));
         HIPCHK(c, hipMalloc(&c->t_mrow, sizeof(uint4) * P));
         HIPCHK(c, hipMemcpy(c->t_mrow, mrow.data(), sizeof(uint4) * P, hipMemcpyHostToDevice));
+        // multi-word split geometry (sparc_movew.hpp): internal pitch + 1, the board plus a
+        // zero row above and one spare dword, the longest possible path in the move stack
+        if (W > 1 && pitch <= 15u) {
+            SplitGeom g{};
+            g.P2 = pitch + 1u;
+            uint32_t xmax = 1, pts = 1;
+            for (size_t q = 0; q < P; ++q) {
+                const uint32_t X = t->info[4 * q] & 0xFFu, Y = (t->info[4 * q] >> 8) & 0xFFu;
+                xmax = std::max(xmax, X);
+                pts = std::max(pts, X * Y);
+            }
+            g.B = ((xmax + 2u) * g.P2 + 31u) / 32u + 1u;
+            g.BS = (g.B + 3u) & ~3u;
+            g.M = c->cfg.traceback ? ((pts - 1u + 15u) & ~15u) : 0u;
+            g.nbr_pos = (2u * g.P2) | ((g.P2 - 1u) << 8) | (0u << 16) | ((g.P2 + 1u) << 24);
+            g.off_board = (uint32_t)kW_Board;
+            g.off_stack = g.off_board + g.BS * 256u;
+            g.pair = (g.off_stack + g.M * 64u + 15u) & ~15u;
+            if (4 * (size_t)g.pair + splitw_fin_bytes() <= kMaxDynLds) {
+                std::vector<uint4> mw(P);
+                std::vector<uint32_t> bw(P * g.BS, 0u);
+                for (size_t q = 0; q < P; ++q) {
+                    const uint32_t* inf = t->info + 4 * q;
+                    const uint32_t X = inf[0] & 0xFF, Y = (inf[0] >> 8) & 0xFF;
+                    const uint32_t sx = (inf[0] >> 16) & 0xFF, sy = inf[0] >> 24;
+                    const uint32_t tx = inf[1] & 0xFF, ty = (inf[1] >> 8) & 0xFF;
+                    mw[q] = make_uint4((sx * g.P2 + sy) | ((tx * g.P2 + ty) << 16), (inf[1] >> 16) & 7u, 0u, 0u);
+                    for (uint32_t x = 0; x < X; ++x)
+                        for (uint32_t y = 0; y < Y; ++y) {
+                            const uint32_t b = x * pitch + y;
+                            if (!((t->open[q * W + (b >> 6)] >> (b & 63)) & 1ull) || (x == sx && y == sy)) continue;
+                            const uint32_t d = (x + 1u) * g.P2 + y;
+                            bw[q * g.BS + (d >> 5)] |= 1u << (d & 31u);
+                        }
+                }
+                HIPCHK(c, hipMalloc(&c->t_mroww, sizeof(uint4) * P));
+                HIPCHK(c, hipMemcpy(c->t_mroww, mw.data(), sizeof(uint4) * P, hipMemcpyHostToDevice));
+                HIPCHK(c, hipMalloc(&c->t_boardw, sizeof(uint32_t) * bw.size()));
+                HIPCHK(c, hipMemcpy(c->t_boardw, bw.data(), sizeof(uint32_t) * bw.size(), hipMemcpyHostToDevice));
+                c->sgeom = g;
+                c->split_w = true;
+            }
+        }
     }
     c->num_puzzles = (uint32_t)t->num_puzzles;
     c->num_nodes = (uint32_t)t->num_nodes;
@@ -1387,6 +1586,43 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
         else go1(std::false_type{});
         if (lds_rc) return lds_rc;
         return launch_check(c);
+    }
+    if (c->W > 1 && !ot && c->split_w && tiled && c->n % 256 == 0 && T >= kTile) {
+        // the full tiles of whole 256-env workgroups go through the multi-word split kernel; a
+        // tail of T % 16 steps through k_rollout below (the state round-trips HBM exactly)
+        const int32_t T16 = T / kTile * kTile;
+        const SplitGeom& g = c->sgeom;
+        const size_t blocks = c->n / 256;
+        const size_t base = 4 * (size_t)g.pair + splitw_fin_bytes();
+        const bool lds_t = base + sizeof(uint4) * c->num_puzzles <= kMaxDynLds;
+        const size_t shm = base + (lds_t ? sizeof(uint4) * c->num_puzzles : 0);
+        dispatch_w_tb(c->W, c->cfg.traceback, [&](auto w, auto tb) {
+            constexpr int W = decltype(w)::value;
+            constexpr bool TB = decltype(tb)::value;
+            if constexpr (W > 1) {
+                auto launch = [&](auto kern, const uint8_t* a) {
+                    if (shm > 64 * 1024 && (lds_rc = allow_big_lds(c, reinterpret_cast<const void*>(kern)))) return;
+                    kern<<<dim3((unsigned)blocks), kBlock1s, shm, c->stream>>>(p, g, c->t_mroww, c->t_boardw, T16, a, seed,
+                                                                              t0, d_rew, d_flags, st);
+                };
+                if (d_act) {
+                    if (lds_t) launch(k_rolloutWs<W, TB, false, true>, d_act);
+                    else launch(k_rolloutWs<W, TB, false, false>, d_act);
+                } else {
+                    if (lds_t) launch(k_rolloutWs<W, TB, true, true>, nullptr);
+                    else launch(k_rolloutWs<W, TB, true, false>, nullptr);
+                }
+            }
+        });
+        if (lds_rc) return lds_rc;
+        rc = launch_check(c);
+        if (rc || T16 == T) return rc;
+        const size_t adv = (size_t)T16 * c->n;
+        if (d_act) d_act += adv;
+        if (d_rew) d_rew += adv;
+        if (d_flags) d_flags += adv;
+        t0 += (uint64_t)T16;
+        T -= T16;
     }
     dispatch_w_tb(c->W, c->cfg.traceback, [&](auto w, auto tb) {
         constexpr int W = decltype(w)::value;

@@ -302,6 +302,83 @@ def test_w1_chunked_partial_workgroups(on_gpu, n):
     _assert_states_equal(b.state(), o.state(), table)
 
 
+@pytest.mark.parametrize("name", ["mixed_5_11", "15x15"])
+@pytest.mark.parametrize("tb", [False, True])
+@pytest.mark.parametrize("max_steps", [12, 2000])
+def test_multiword_split_chunked_vs_oracle(on_gpu, name, tb, max_steps):
+    """W = 2 / 4 rollouts at n = 2560 (whole 256-env workgroups): the full tiles run through the
+    multi-word split kernel k_rolloutWs (free board in LDS, TrieLane trie wave), the T % 16
+    tails through the generic k_rollout.  Launches of 100 + 57 + 1 + 32 steps equal one launch
+    of 190 (reward codes, flags, stats) and the oracle, also with many autoresets per launch
+    (max_steps 12) and illegal actions."""
+    from sparc_gym_amd import SPaRCVecEnv
+    proc, table = _make(name, seed=31 + max_steps)
+    assert table.words > 1
+    n = 2560
+    pids = (np.arange(n) * 7) % len(proc)
+    rng = np.random.default_rng(max_steps + 17 * tb)
+    acts_np = rng.choice(np.array([0, 1, 2, 3, 0, 1, 2, 3, 4, 255], np.uint8), size=(190, n))
+    acts = torch.from_numpy(acts_np).cuda()
+    kw = dict(processed=proc, table=table, traceback=tb, observation="compact", max_steps=max_steps)
+    a = SPaRCVecEnv(n, **kw)
+    a.reset(options={"puzzle_index": pids})
+    sa = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
+    full = a.rollout(190, acts, stats=sa)
+    b = SPaRCVecEnv(n, **kw)
+    b.reset(options={"puzzle_index": pids})
+    sb = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
+    parts, t = [], 0
+    for T in (100, 57, 1, 32):
+        parts.append(b.rollout(T, acts[t:t + T].contiguous(), stats=sb))
+        t += T
+    for key in ("reward_code", "flags"):
+        assert torch.equal(full[key], torch.cat([p[key] for p in parts]))
+    assert torch.equal(sa, sb)
+    o = COracle(oracle_pool_from_processed(proc), n, tb, max_steps, autoreset=1)
+    o.reset(pids)
+    ost = np.zeros((n, 4), np.int32)
+    ro, fo = o.rollout(190, acts_np, stats=ost)
+    assert np.array_equal(full["reward_code"].cpu().numpy(), ro)
+    assert np.array_equal(full["flags"].cpu().numpy(), fo)
+    assert np.array_equal(sa.cpu().numpy(), ost)
+    _assert_states_equal(a.state(), o.state(), table)
+    _assert_states_equal(b.state(), o.state(), table)
+    if max_steps == 12:
+        assert ost[:, 3].sum() > n       # autoresets inside the launches
+
+
+def test_multiword_full_size_15x15_vs_oracle(on_gpu):
+    """The second reading of '7x7' (SPaRC_Gym.py:243-248): a 7x7 cell grid = 15x15 lattice on
+    4-word boards, 65,536 envs, traceback, full property set (bench config c3g7): bit-exact
+    against the C oracle and the size-independent invariants."""
+    from sparc_gym_amd import SPaRCVecEnv
+    recs = synthetic.make_puzzles(1024, seed=0, sizes=((7, 7),), full_properties=True)
+    proc = process_puzzles(recs)
+    table = pack_table(proc)
+    assert table.words == 4
+    n, T = 65536, 208
+    pids = (np.arange(n, dtype=np.uint64) * 2654435761 % 1024).astype(np.int64)
+    v = SPaRCVecEnv(n, processed=proc, table=table, traceback=True, observation="compact")
+    v.reset(options={"puzzle_index": pids})
+    stats = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
+    out = v.rollout(T, None, seed=77, stats=stats)
+    r, f = out["reward_code"].cpu().numpy(), out["flags"].cpu().numpy()
+    st = stats.cpu().numpy()
+    assert np.array_equal(st[:, 0], r.astype(np.int64).sum(0))
+    assert np.array_equal(st[:, 1], ((f & 3) != 0).sum(0))
+    s = v.state()
+    pop = np.zeros(n, np.int64)
+    for w in range(table.words):
+        pop += np.array([bin(int(b)).count("1") for b in s["visited"][w]])
+    assert np.array_equal(pop, s["path_len"].astype(np.int64))
+    o = COracle(oracle_pool_from_processed(proc), n, True, 2000, autoreset=1)
+    o.reset(pids)
+    ost = np.zeros((n, 4), np.int32)
+    ro, fo = o.rollout(T, None, seed=77, stats=ost)
+    assert np.array_equal(r, ro) and np.array_equal(f, fo)
+    assert np.array_equal(st, ost)
+
+
 def test_w1_rollout_without_outputs_keeps_state_and_stats(on_gpu):
     """record=False (no reward / flag tensors) and in-kernel random actions: same state and
     stats as the recorded run."""
@@ -323,13 +400,14 @@ def test_w1_rollout_without_outputs_keeps_state_and_stats(on_gpu):
     assert np.array_equal(runs[0][1]["visited"], runs[1][1]["visited"])
 
 
-@pytest.mark.parametrize("max_steps", [3, 9, 25])
-def test_many_short_episodes_vs_oracle(on_gpu, max_steps):
+@pytest.mark.parametrize("max_steps,sizes", [(3, ((3, 3),)), (9, ((3, 3),)), (25, ((3, 3),)),
+                                             (9, ((7, 7),)), (25, ((4, 4), (5, 5)))])
+def test_many_short_episodes_vs_oracle(on_gpu, max_steps, sizes):
     """Thousands of autoresets per launch (short max_steps, puzzles with many solutions sharing
     prefixes, mostly-legal actions): every done step's reward and the step after it are where
     the pipelined rollout hands the trie state over to the reset, so compare them all."""
     from sparc_gym_amd import SPaRCVecEnv
-    recs = synthetic.make_puzzles(256, seed=max_steps, sizes=((3, 3),), n_solutions=8,
+    recs = synthetic.make_puzzles(256, seed=max_steps, sizes=sizes, n_solutions=8,
                                   shared_prefix_prob=0.9, full_properties=False)
     proc = process_puzzles(recs)
     table = pack_table(proc)
