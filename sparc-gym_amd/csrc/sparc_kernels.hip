@@ -740,9 +740,9 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
             stats[i] = st;
         }
     } else {                                                     // ---- trie waves
-        // the trie wave wins VALU arbitration against its (older) move wave partner: its chain
-        // carries the record-gather waits, the move wave has slack (c3: 0.289 -> 0.266 ms per
-        // 1,000 steps; priority to the move wave instead: no change)
+        // the trie wave wins VALU arbitration against its (older) move wave partner (c3: 0.289
+        // -> 0.266 ms per 1,000 steps with the earlier trie wave; with TrieLane, 2,000 steps:
+        // 0.456 ms, 0.476 without priority, 0.477 with the move wave at 1 instead)
         __builtin_amdgcn_s_setprio(1);
         TrieLane tl;
         tl.load(p.st.pos[i], p.st.aux[i], p.st.pid[i], trow, p.tab.trie8, NP);
@@ -887,7 +887,9 @@ __global__ void __launch_bounds__(kBlock1s) k_rolloutWs(Params p, SplitGeom g, c
             stats[i] = st;
         }
     } else {                                                     // ---- trie waves
-        __builtin_amdgcn_s_setprio(1);
+        // no priority here: with the board in LDS the move wave's chain is the longer one
+        // (MI355X, c3g7: 0.613 ms per 2,000-step launch with the trie wave at s_setprio 1,
+        // 0.558 without, 0.561 with the move wave at 1)
         TrieLane tl;
         tl.load(p.st.pos[i], p.st.aux[i], p.st.pid[i], trow, p.tab.trie8, NP);
         const uint16_t* th = reinterpret_cast<const uint16_t*>(pb + kW_Hand) + lane;
