@@ -458,8 +458,8 @@ struct Env<1, TB, Stack> {
     // solutions, done, reset step
     uint32_t s_a = 0, s_fwd = 0, s_pop = 0, s_mv = 0, s_done = 0, s_rs = 0;
     uint4 rec;
-    // k_rollout1s move wave: the next puzzle's index, row word and reset board, loaded at the
-    // previous reset (reset_next_pf)
+    // k_rollout1s move wave: the row word and reset board of the puzzle the next autoreset
+    // loads, and the index of the one after it, read at the previous reset (reset_next_m)
     uint32_t rpid = 0, rrow = 0;
     uint64_t rinit = 0;
 
@@ -556,16 +556,16 @@ struct Env<1, TB, Stack> {
     // move wave): they were read at the previous reset (or at load), so a reset waits on no
     // read (MI355X, c3: 0.466 -> 0.460 ms per 2,000-step launch); a resetting lane then reads
     // the row of the puzzle after the new one, for its next reset.  Move rows (split kernel):
-    // {row1.x, reset board lo, hi, 0}.
-    __device__ __forceinline__ void prefetch_reset_m(const uint4* mrow, uint32_t num_puzzles) {
-        rpid = pid + 1 == num_puzzles ? 0u : pid + 1;
-        const uint4 m = mrow[rpid];
+    // {row1.x, reset board lo, hi, the index of the puzzle after it}.  The move wave does not
+    // track the puzzle index (the trie wave does, and hands it over at the end).
+    __device__ __forceinline__ void prefetch_reset_m(const uint4* mrow, uint32_t q) {
+        const uint4 m = mrow[q];
         rrow = m.x;
         rinit = ((uint64_t)m.z << 32) | m.y;
+        rpid = m.w;
     }
     __device__ __forceinline__ void reset_next_m(const Params& p, const uint4* mrow) {
         if (pending & (uint32_t)(p.autoreset == 1)) {
-            pid = rpid;
             e = rrow & 0xFFu;
             tgt = (rrow >> 8) & 0xFFu;
             pflags = rrow >> 16;
@@ -574,7 +574,7 @@ struct Env<1, TB, Stack> {
             len = 1;
             step = -1;   // this step's increment brings it to 0
             rs = 1;
-            prefetch_reset_m(mrow, p.tab.num_puzzles);
+            prefetch_reset_m(mrow, rpid);
         }
     }
     __device__ __forceinline__ uint32_t phase_move(const Params& p, uint32_t a) {

@@ -605,8 +605,8 @@ __global__ void __launch_bounds__(kBlock1) k_rollout1(Params p, int32_t T, const
 // k_rollout1.  The state after the launch is the same SoA record (the trie wave hands its
 // final trie state and counters to the move wave through LDS before the store).
 constexpr int kBlock1s = 768;
-constexpr size_t kS_Act = 0;                          // actions [2 tiles][16][64]
-constexpr size_t kS_Rew = kS_Act + 2 * kTile * 64;    // reward ring [64 steps][64]
+constexpr size_t kS_Act = 0;                          // actions [3 tiles][16][64]
+constexpr size_t kS_Rew = kS_Act + 3 * kTile * 64;    // reward ring [64 steps][64]
 constexpr size_t kS_FH = kS_Rew + kRing * 64;         // hand-over ring [64 steps][64] u32
 constexpr size_t kS_Stk = kS_FH + 4 * kRing * 64;     // move stack [64 moves][64]
 constexpr size_t kS_Pair = kS_Stk + 64 * 64;          // per move / trie wave pair
@@ -615,10 +615,10 @@ constexpr size_t kS_Base = kS_Fin + 4 * 64 * 2 * sizeof(uint4);
 // LDS bytes of the staged rows: move rows + trie rows, 16 B each per puzzle
 __host__ __device__ constexpr size_t split_table_bytes(uint32_t P) { return (size_t)P * 2 * sizeof(uint4); }
 
-// the flag bytes (byte 1) of four hand-over words
+// the flag bytes (byte 0) of four hand-over words
 __device__ __forceinline__ uint32_t flag_bytes4(const u32x4 w) {
-    const uint32_t lo = __builtin_amdgcn_perm(w.y, w.x, 0x0C0C0501u);
-    const uint32_t hi = __builtin_amdgcn_perm(w.w, w.z, 0x0C0C0501u);
+    const uint32_t lo = __builtin_amdgcn_perm(w.y, w.x, 0x0C0C0400u);
+    const uint32_t hi = __builtin_amdgcn_perm(w.w, w.z, 0x0C0C0400u);
     return lo | (hi << 16);
 }
 
@@ -653,10 +653,10 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         // issue load sat on one SIMD (MI355X, c3: 0.468 -> 0.466 ms per launch with four)
         const uint32_t io = wv - 8u;
         const uint32_t r = lane >> 2, c = (lane & 3u) * 16u;
-        auto load_tile = [&](int32_t k) {                        // actions of tile k -> buffer k & 1
+        auto load_tile = [&](int32_t k) {                        // actions of tile k -> buffer k % 3
             if constexpr (!RAND) {
                 const u32x4 v = nt_load16(act + (size_t)(k * kTile + r) * n + wg_base + io * 64 + c);
-                *reinterpret_cast<u32x4*>(smem + io * kS_Pair + kS_Act + (k & 1) * (kTile * 64) + r * 64 + c) = v;
+                *reinterpret_cast<u32x4*>(smem + io * kS_Pair + kS_Act + (k % 3) * (kTile * 64) + r * 64 + c) = v;
             }
         };
         auto store_tile = [&](int32_t k) {                       // whole 128-B lines, as k_rollout1
@@ -667,7 +667,7 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
             const uint8_t* base = smem + w * kS_Pair + row * 64 + (c8 & 63u);
             const size_t o = (size_t)(k * kTile + h * 8 + r8) * n + wg_base + q * 128 + c8;
             if (rew) nt_store16(reinterpret_cast<uint8_t*>(rew) + o, *reinterpret_cast<const u32x4*>(base + kS_Rew));
-            if (flg) {   // byte 1 of 16 hand-over words
+            if (flg) {   // byte 0 of 16 hand-over words
                 const u32x4* fh = reinterpret_cast<const u32x4*>(smem + w * kS_Pair + kS_FH + row * 256 + 4 * (c8 & 63u));
                 u32x4 v;
                 v.x = flag_bytes4(fh[0]);
@@ -698,25 +698,32 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         Env<1, TB, typename std::conditional<TB, LdsStack<64>, RegStack>::type> e;
         if constexpr (TB) e.stk.col = pb + kS_Stk + lane;
         e.load(p, src, i);
-        e.prefetch_reset_m(mrow, NP);
+        e.prefetch_reset_m(mrow, e.pid + 1 == NP ? 0u : e.pid + 1);
         const uint32_t pend0 = e.pending;
         const uint64_t gid = p.env_offset + i;
         uint32_t* th = reinterpret_cast<uint32_t*>(pb + kS_FH) + lane;
         __syncthreads();                                         // B_0
         for (int32_t k = 0; k < K; ++k) {
-            const uint8_t* ta = pb + kS_Act + (k & 1) * (kTile * 64) + lane;
+            // tile k's actions (buffer k % 3; the trie wave reads them one tile later)
+            uint8_t* ta = pb + kS_Act + (k % 3) * (kTile * 64) + lane;
 #pragma unroll 1
             for (int g = 0; g < kTile; g += 4) {
                 uint32_t av[4];
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    av[j] = RAND ? uint_rand_action(seed, gid, t0 + (uint64_t)(k * kTile + g + j)) : ta[(g + j) * 64];
+                for (int j = 0; j < 4; ++j) {
+                    if constexpr (RAND) {
+                        av[j] = uint_rand_action(seed, gid, t0 + (uint64_t)(k * kTile + g + j));
+                        ta[(g + j) * 64] = (uint8_t)av[j];
+                    } else {
+                        av[j] = ta[(g + j) * 64];
+                    }
+                }
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const uint32_t row = (uint32_t)(k * kTile + g + j) & (kRing - 1);
                     e.reset_next_m(p, mrow);
                     const uint32_t f = e.phase_move(p, av[j]);
-                    th[row * 64] = hand_word32(e.s_a, e.s_fwd, e.s_pop, f, e.s_done, e.s_mv);
+                    th[row * 64] = hand_word32(e.s_fwd, e.s_pop, f);
                 }
             }
             __syncthreads();                                     // B_{k+1}
@@ -728,6 +735,7 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         e.nn = fs.x & 0xFFFFu;
         e.off = fs.x >> 16;
         e.outcome = e.pending ? (fs.y == 0u ? 1u : 2u) : 0u;   // outcome_reward after the last step
+        e.pid = fc.y;
         e.store(p, src, i);
         if (stats) {
             // autoresets: one per done step before the last, plus one for a done step carried in
@@ -751,20 +759,24 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         __syncthreads();                                         // B_0
         __syncthreads();                                         // B_1 (interval 0: no tile yet)
         for (int32_t k = 1; k <= K; ++k) {
+            const uint8_t* ta = pb + kS_Act + ((k - 1) % 3) * (kTile * 64) + lane;   // tile k-1's actions
 #pragma unroll 1
             for (int g = 0; g < kTile; g += 4) {
-                // the group's 4 hand-over words first (one LDS wait), then its 4 steps
+                // the group's 4 hand-over words and actions first (one LDS wait), then its 4 steps
                 const uint32_t row0 = (uint32_t)((k - 1) * kTile + g) & (kRing - 1);
-                uint32_t hb[4];
+                uint32_t hb[4], av[4];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) hb[j] = th[(row0 + j) * 64];
+                for (int j = 0; j < 4; ++j) {
+                    hb[j] = th[(row0 + j) * 64];
+                    av[j] = ta[(g + j) * 64];
+                }
 #pragma unroll
-                for (int j = 0; j < 4; ++j) tr[(row0 + j) * 64] = (uint8_t)tl.step(hb[j], trow, p.tab.trie8, NP);
+                for (int j = 0; j < 4; ++j) tr[(row0 + j) * 64] = (uint8_t)tl.step(hb[j], av[j], trow, p.tab.trie8, NP);
             }
             __syncthreads();                                     // B_{k+1}
         }
         fin[0] = make_uint4(tl.S, (uint32_t)tl.Oneg, (uint32_t)tl.acc_x, tl.acc_z);
-        fin[1] = make_uint4(tl.acc_y, 0u, 0u, 0u);
+        fin[1] = make_uint4(tl.acc_y, tl.pid, 0u, 0u);
         __syncthreads();                                         // B_{K+2}
     }
 }
@@ -818,14 +830,14 @@ __global__ void __launch_bounds__(kBlock1s) k_rolloutWs(Params p, SplitGeom g, c
             const uint8_t* base = smem + w * g.pair + row * 64 + (c8 & 63u);
             const size_t o = (size_t)(k * kTile + h * 8 + r8) * n + wg_base + q * 128 + c8;
             if (rew) nt_store16(reinterpret_cast<uint8_t*>(rew) + o, *reinterpret_cast<const u32x4*>(base + kW_Rew));
-            if (flg) {   // byte 1 of 16 u16 hand-over words
+            if (flg) {   // byte 0 of 16 u16 hand-over words
                 const u32x4* fh = reinterpret_cast<const u32x4*>(smem + w * g.pair + kW_Hand + row * 128 + 2 * (c8 & 63u));
                 const u32x4 a = fh[0], b = fh[1];
                 u32x4 v;
-                v.x = __builtin_amdgcn_perm(a.y, a.x, 0x07050301u);
-                v.y = __builtin_amdgcn_perm(a.w, a.z, 0x07050301u);
-                v.z = __builtin_amdgcn_perm(b.y, b.x, 0x07050301u);
-                v.w = __builtin_amdgcn_perm(b.w, b.z, 0x07050301u);
+                v.x = __builtin_amdgcn_perm(a.y, a.x, 0x06040200u);
+                v.y = __builtin_amdgcn_perm(a.w, a.z, 0x06040200u);
+                v.z = __builtin_amdgcn_perm(b.y, b.x, 0x06040200u);
+                v.w = __builtin_amdgcn_perm(b.w, b.z, 0x06040200u);
                 nt_store16(flg + o, v);
             }
         };
@@ -867,7 +879,7 @@ __global__ void __launch_bounds__(kBlock1s) k_rolloutWs(Params p, SplitGeom g, c
                     const uint32_t row = (uint32_t)(k * kTile + gq + j) & (kRing - 1);
                     m.reset_next(p, g, mrow, boards);
                     const uint32_t f = m.phase_move(p, g, av[j]);
-                    th[row * 64] = (uint16_t)hand_word16(m.s_a, m.s_fwd, m.s_pop, f, m.s_done, m.s_mv);
+                    th[row * 64] = (uint16_t)hand_word16(m.s_a, m.s_fwd, m.s_pop, f);
                 }
             }
             __syncthreads();                                     // B_{k+1}
@@ -905,7 +917,8 @@ __global__ void __launch_bounds__(kBlock1s) k_rolloutWs(Params p, SplitGeom g, c
                 for (int j = 0; j < 4; ++j) hb[j] = th[(row0 + j) * 64];
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
-                    tr[(row0 + j) * 64] = (uint8_t)tl.step(widen_hand_word(hb[j]), trow, p.tab.trie8, NP);
+                    tr[(row0 + j) * 64] = (uint8_t)tl.step(widen_hand_word(hb[j]), __builtin_amdgcn_ubfe(hb[j], 10u, 2u),
+                                                           trow, p.tab.trie8, NP);
             }
             __syncthreads();                                     // B_{k+1}
         }
@@ -1385,8 +1398,10 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
             // flags as row1: bit0 solutions, bit1 root valid, bit3 root terminal
             const uint32_t tf = (fl & 3u) | (((dinfo[q].y >> 19) & 1u) << 3);
             const uint32_t rootS = (tf & 2u) ? ((tf >> 3) & 1u) << 15 : 0x10000u;
-            trow[q] = make_uint4(rr.x, rr.y, inf[2], rootS | ((cnt ? cnt - 1u : 0u) << 17));
-            if (W == 1) mrow[q] = make_uint4(row1[q].x, (uint32_t)init[q], (uint32_t)(init[q] >> 32), 0u);
+            trow[q] = make_uint4(rr.x, rr.y, inf[2], rootS | ((tf & 1u) << 14) | ((cnt ? cnt - 1u : 0u) << 17));
+            // W = 1 move row: row word, reset board, and the puzzle the autoreset after it loads
+            if (W == 1) mrow[q] = make_uint4(row1[q].x, (uint32_t)init[q], (uint32_t)(init[q] >> 32),
+                                             q + 1 == P ? 0u : (uint32_t)q + 1u);
         }
         HIPCHK(c, hipMalloc(&c->t_trie8, sizeof(uint2) * nn));
         HIPCHK(c, hipMemcpy(c->t_trie8, t8.data(), sizeof(uint2) * nn, hipMemcpyHostToDevice));

@@ -38,15 +38,14 @@ struct SplitGeom {
     uint32_t off_board, off_stack;   // their offsets within a pair
 };
 
-// 16-bit hand-over word of the multi-word kernel: bit0 moved on a puzzle with solutions, bit1
-// done, bits 2-3 fwd - pop + 1, bits 4-5 action & 3, bits 8-15 the flag byte.  The trie wave
-// widens it to TrieLane's 32-bit word (fwd - pop in bits 16-31).
-__device__ __forceinline__ uint32_t hand_word16(uint32_t a, uint32_t fwd, uint32_t pop, uint32_t f, uint32_t done,
-                                                uint32_t mvs) {
-    return ((a & 3u) << 4) | (f << 8) | ((fwd + 1u - pop) << 2) | (done << 1) | mvs;
+// 16-bit hand-over word of the multi-word kernel: bits 0-7 the flag byte, bits 8-9
+// fwd - pop + 1, bits 10-11 action & 3.  The trie wave widens it to TrieLane's word (flag byte
+// | (fwd - pop) << 8) and the action.
+__device__ __forceinline__ uint32_t hand_word16(uint32_t a, uint32_t fwd, uint32_t pop, uint32_t f) {
+    return f | ((fwd + 1u - pop) << 8) | ((a & 3u) << 10);
 }
 __device__ __forceinline__ uint32_t widen_hand_word(uint32_t h) {
-    return (h & 0xFF33u) | ((__builtin_amdgcn_ubfe(h, 2u, 2u) - 1u) << 16);
+    return (h & 0xFFu) | ((__builtin_amdgcn_ubfe(h, 8u, 2u) - 1u) << 8);
 }
 
 template <bool TB>

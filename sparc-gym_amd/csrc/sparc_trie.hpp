@@ -3,15 +3,13 @@
 // The solution-prefix test of step() (_is_on_solution_path, SPaRC_Gym.py:1244-1265, and the
 // np.array_equal test of 1206) walks a per-puzzle trie of the solution paths.  It needs from
 // the move wave only what the move did, so in the split kernels a TRIE wave runs it one tile
-// behind the move wave of the same 64 envs, from a 32-bit hand-over word per env-step:
+// behind the move wave of the same 64 envs, from a 32-bit hand-over word per env-step and the
+// step's action (which the trie wave reads from the action tile itself):
 //
-//   bit   0     moved on a puzzle with solutions (the +-1 reward applies, 1217)
-//   bit   1     done = terminated or truncated
-//   bits  4-5   action & 3      (hw & 0x30 is the field offset a * 16)
-//   bits  8-15  the flag byte   term | trunc << 1 | legal << 2 | autoreset << 6
-//   bits 16-31  fwd - pop       (+1 forward move, -1 traceback pop, 0 no move; 16-bit two's
-//                                complement, so adding hw & 0xFFFF0000 adds it to S's off field,
-//                                and bit 16 = moved)
+//   bits  0-7   the flag byte   term | trunc << 1 | legal << 2 | autoreset << 6
+//   bits  8-31  fwd - pop       (+1 forward move, -1 traceback pop, 0 no move), two's complement
+//
+// so the move wave packs two fields (the flag byte it outputs anyway, and the move).
 //
 // Geometry-independent: the same lane serves the W = 1 and the multi-word kernels.
 //
@@ -34,14 +32,15 @@
 namespace sparc {
 
 // per puzzle trie row: {root children right | up << 16, root children left | down << 16,
-// trie base, root S | trie max << 17}; root S = 0 or 0x8000 ([start] itself a solution) when
-// some solution starts at start, else 0x10000 (off the trie from the start).  Rootless:
-// children 0xFFFF.
+// trie base, root S | has solutions << 14 | trie max << 17}; root S = 0 or 0x8000 ([start]
+// itself a solution) when some solution starts at start, else 0x10000 (off the trie from the
+// start).  Rootless: children 0xFFFF.
 struct TrieLane {
     uint32_t S = 0;
     int32_t Oneg = -100;
     uint32_t rx = ~0u, ry = ~0u;   // record of the current node (S & 0x7FFF)
     uint32_t base = 0, tmax = 0;
+    int32_t hs = 0;                 // the puzzle has solutions (the +-1 rewards apply, 1217)
     uint32_t pid = 0, npid = 0;
     uint4 nx;                       // trie row of npid, read at the previous reset
     int acc_x = 0;                  // sum of reward codes
@@ -60,6 +59,7 @@ struct TrieLane {
         const uint4 r = trow[q];
         base = r.z;
         tmax = r.w >> 17;
+        hs = (int32_t)((r.w >> 14) & 1u);
         S = ((ps >> 24) << 16) | (ax & 0x7FFFu) | (((ax >> 19) & 1u) << 15);
         Oneg = ((ax >> 16) & 3u) == 1u ? 0 : -100;
         if ((r.w & 0x10000u) == 0u) {   // rootless puzzles keep off >= 1: the record is never read
@@ -72,17 +72,18 @@ struct TrieLane {
         nx = trow[npid];
     }
 
-    // one env-step from its hand-over word; returns the reward code (x100, 1201-1223)
+    // one env-step from its hand-over word and action; returns the reward code (x100, 1201-1223)
     template <class Rows>
-    __device__ __forceinline__ int step(const uint32_t hw, const Rows& trow, const uint2* __restrict__ trie8,
-                                        uint32_t num_puzzles) {
-        if (hw & 0x4000u) {   // autoreset step: the next puzzle's rows and its trie root
+    __device__ __forceinline__ int step(const uint32_t hw, const uint32_t a, const Rows& trow,
+                                        const uint2* __restrict__ trie8, uint32_t num_puzzles) {
+        if (hw & 0x40u) {   // autoreset step: the next puzzle's rows and its trie root
             pid = npid;
             npid = next_pid(npid, num_puzzles);
             rx = nx.x;
             ry = nx.y;
             base = nx.z;
-            S = nx.w & 0x1FFFFu;
+            S = nx.w & 0x18000u;
+            hs = (int32_t)((nx.w >> 14) & 1u);
             tmax = nx.w >> 17;
         }
         // the row of the next reset, read every step outside the branch: read inside it, the
@@ -92,10 +93,11 @@ struct TrieLane {
         // bits above 15 set when the lane is off the trie or did not move, so one compare
         // decides; off the trie (or without a child) the move counts the depth instead.
         const uint64_t xy = ((uint64_t)ry << 32) | rx;
-        const uint32_t c = (uint32_t)(xy >> (hw & 0x30u));
-        const uint32_t key = __builtin_amdgcn_ubfe(c, 0u, 16u) | (S & 0xFFFF0000u) | (~hw & 0x10000u);
+        const uint32_t c = (uint32_t)(xy >> ((a << 4) & 0x30u));
+        const uint32_t dd = (hw << 8) & 0xFFFF0000u;           // (fwd - pop) << 16; bit 16: moved
+        const uint32_t key = __builtin_amdgcn_ubfe(c, 0u, 16u) | (S & 0xFFFF0000u) | (~dd & 0x10000u);
         const bool take = key < 0xFFFFu;
-        S = take ? key : S + (hw & 0xFFFF0000u);
+        S = take ? key : S + dd;
         // the record changes only with the node (exec-masked gather; a random walk is off the
         // trie on most steps)
         if (take) {
@@ -109,21 +111,20 @@ struct TrieLane {
         // nor is done)
         const uint32_t x = S >> 15;                            // 0 on, 1 on a solution, >= 2 off
         const int cd = x == 1u ? 100 : Oneg;
-        const int cm = __mul24(x < 2u ? 1 : -1, (int)(hw & 1u));
-        const uint32_t done = __builtin_amdgcn_ubfe(hw, 1u, 1u);
+        const int cm = hw >= 0x100u ? (x < 2u ? hs : -hs) : 0;
+        const bool done = (hw & 3u) != 0u;
         const int code = done ? cd : cm;
         Oneg = done ? (cd < 0 ? cd : 0) : -100;
         acc_x += code;
-        acc_y += done;
+        acc_y += (uint32_t)done;
         acc_z += (uint32_t)(code == 100);
         return code;
     }
 };
 
 // the move wave's side of the hand-over word (see above)
-__device__ __forceinline__ uint32_t hand_word32(uint32_t a, uint32_t fwd, uint32_t pop, uint32_t f, uint32_t done,
-                                                uint32_t mvs) {
-    return ((a & 3u) << 4) | (f << 8) | ((fwd - pop) << 16) | (done << 1) | mvs;
+__device__ __forceinline__ uint32_t hand_word32(uint32_t fwd, uint32_t pop, uint32_t f) {
+    return ((fwd - pop) << 8) | f;
 }
 
 }  // namespace sparc
