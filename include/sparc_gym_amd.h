@@ -186,6 +186,15 @@ int sparc_rollout_obs_device(void *ctx, int32_t T, const uint8_t *d_actions, uin
                              int8_t *d_reward, uint8_t *d_flags, int32_t *d_stats, int32_t *d_visited,
                              int32_t *d_agent, int32_t x_dim, int32_t y_dim);
 
+/* sparc_rollout_device that also runs the rule audit after every step, as the reference's
+ * step() does (_validate_rules at SPaRC_Gym.py:1227 and again in _get_info 1011, filling
+ * info['rule_status'], 941-950): d_rule_bits [T][N] uint16, step t's entry equal to
+ * sparc_rules_device's bits after the t-th of T single steps.  Needs sparc_load_rules.  The
+ * audit (flood fills, exact-fit searches) costs far more than the step; this path runs the
+ * generic per-wave kernel. */
+int sparc_rollout_rules_device(void *ctx, int32_t T, const uint8_t *d_actions, uint64_t seed, uint64_t t0,
+                               int8_t *d_reward, uint8_t *d_flags, int32_t *d_stats, uint16_t *d_rule_bits);
+
 int sparc_read_state(void *ctx, const sparc_state_host *out);
 /* device-to-device copy of one SoA state array (`which` as in sparc_state_ptr) into d_out,
  * ordered on the context's stream (e.g. the per-env puzzle index after autoresets). */

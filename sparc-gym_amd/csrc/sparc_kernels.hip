@@ -270,11 +270,18 @@ struct ObsTrace {
     int32_t* aout;
     uint32_t XD, YD;
 };
-template <int W, bool TB, bool RAND, bool LDS_TABLE, int EPW, bool OBS = false>
+// RULES: after every step the wave also runs the rule audit of every env's new state
+// (_validate_rules, which the reference's step() runs every step, SPaRC_Gym.py:1227 / 1011) and
+// writes its bits to bits + t * N ([T][N] uint16, as sparc_rules_device's bits)
+struct RuleTrace {
+    RulesTab rt;
+    uint16_t* bits;
+};
+template <int W, bool TB, bool RAND, bool LDS_TABLE, int EPW, bool OBS = false, bool RULES = false>
 __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const uint8_t* __restrict__ act,
                                                     uint64_t seed, uint64_t t0, int8_t* __restrict__ rew,
                                                     uint8_t* __restrict__ flg, int4* __restrict__ stats,
-                                                    uint32_t tiled, ObsTrace ot) {
+                                                    uint32_t tiled, ObsTrace ot, RuleTrace rtr) {
     static_assert(!OBS || EPW == 64, "the observation writer needs full 64-lane waves");
     constexpr int kUnrollSteps = OBS ? 1 : 4;   // OBS: one step body (its plane writer is long)
     // LDS: [I/O tiles, 3*16*EPW B per wave][W=1 traceback: move stacks, 64*EPW B per wave][rows]
@@ -345,12 +352,25 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
                         ot.aout ? ot.aout + run : nullptr);
         }
     };
+    auto audit_step = [&](int32_t t) {               // rule bits of the state after step t
+        if constexpr (RULES) {
+            uint64_t v[W];
+            uint32_t ab;
+            e.obs_words(p, src, v, ab);
+            BB<W> vb;
+#pragma unroll
+            for (int k = 0; k < W; ++k) vb.w[k] = v[k];
+            const uint32_t xy = e.agent_xy(p);
+            const RuleOut<W> ro = audit<W>(p, rtr.rt, vb, xy & 0xFFu, (xy >> 8) & 0xFFu, e.pid, nullptr);
+            rtr.bits[(size_t)t * n + i] = (uint16_t)ro.bits;
+        }
+    };
     u32x4 anext = {0u, 0u, 0u, 0u};
-    if (!RAND && full && T >= kTile) anext = nt_load16(act + (size_t)r * n + wave_base + c);
+    if (!RAND && !RULES && full && T >= kTile) anext = nt_load16(act + (size_t)r * n + wave_base + c);
 
     for (int32_t tb = 0; tb < T; tb += kTile) {
         const int32_t cnt = T - tb < kTile ? T - tb : kTile;
-        if (full && cnt == kTile) {
+        if (!RULES && full && cnt == kTile) {
             if constexpr (!RAND) {
                 const u32x4 acur = anext;
                 if (tb + 2 * kTile <= T) anext = nt_load16(act + (size_t)(tb + kTile + r) * n + wave_base + c);
@@ -404,6 +424,7 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
                     acc.y += (f & 3u) ? 1 : 0;
                     acc.z += ((f & 3u) && code == 100) ? 1 : 0;
                     acc.w += (f & 64u) ? 1 : 0;
+                    audit_step(t);
                 }
                 obs(t);
             }
@@ -1527,7 +1548,7 @@ int sparc_step_host(void* ctx, const uint8_t* act, int8_t* rew, uint8_t* flags) 
 namespace {
 // sparc_rollout_device / sparc_rollout_obs_device; `ot` non-null: observation traces
 int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_t t0, int8_t* d_rew,
-                 uint8_t* d_flags, int32_t* d_stats, const ObsTrace* ot) {
+                 uint8_t* d_flags, int32_t* d_stats, const ObsTrace* ot, const RuleTrace* rtr = nullptr) {
     int rc = check_ctx(c, true);
     if (rc) return rc;
     if (T < 0) return fail(c, SPARC_E_INVALID, "T must be >= 0");
@@ -1535,6 +1556,7 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
     if ((uint64_t)T * c->n > (1ull << 40)) return fail(c, SPARC_E_INVALID, "T*N too large");
     const Params p = make_params(c);
     const ObsTrace no_obs{nullptr, nullptr, 1u, 1u};
+    const RuleTrace no_rules{RulesTab{}, nullptr};
     int lds_rc = SPARC_OK;   // allow_big_lds failure inside a launch lambda (then no launch)
     int4* st = reinterpret_cast<int4*>(d_stats);
     auto aligned = [](const void* q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & 15u) == 0; };
@@ -1544,7 +1566,7 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
     // envs per wave: 64.  (Measured on MI355X at 65,536 envs: 32-wide waves, two per SIMD, are
     // 1.3x slower than one full wave per SIMD — a half-empty wave costs the full issue time.)
     const bool half = false;
-    if (c->W == 1 && !ot) {
+    if (c->W == 1 && !ot && !rtr) {
         const size_t blocks = (c->n + 255) / 256;
         const size_t per_cu = (blocks + 255) / 256;
         const size_t budget = std::min(kMaxDynLds, (size_t)160 * 1024 / (per_cu ? per_cu : 1));
@@ -1604,7 +1626,7 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
         if (lds_rc) return lds_rc;
         return launch_check(c);
     }
-    if (c->W > 1 && !ot && c->split_w && tiled && c->n % 256 == 0 && T >= kTile) {
+    if (c->W > 1 && !ot && !rtr && c->split_w && tiled && c->n % 256 == 0 && T >= kTile) {
         // the full tiles of whole 256-env workgroups go through the multi-word split kernel; a
         // tail of T % 16 steps through k_rollout below (the state round-trips HBM exactly)
         const int32_t T16 = T / kTile * kTile;
@@ -1644,10 +1666,11 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
     dispatch_w_tb(c->W, c->cfg.traceback, [&](auto w, auto tb) {
         constexpr int W = decltype(w)::value;
         constexpr bool TB = decltype(tb)::value;
-        auto go = [&](auto epw_c, auto obs_c) {
+        auto go = [&](auto epw_c, auto obs_c, auto rules_c) {
             constexpr int EPW = decltype(epw_c)::value;
             constexpr bool OBS = decltype(obs_c)::value;
-            if constexpr (W == 1 && !OBS) return;   // k_rollout1 above
+            constexpr bool RULES = decltype(rules_c)::value;
+            if constexpr (W == 1 && !OBS && !RULES) return;   // k_rollout1 above
             const size_t blocks = (c->n + kWaves * EPW - 1) / (kWaves * EPW);
             const size_t per_cu = (blocks + 255) / 256;
             const size_t budget = std::min(kMaxDynLds, (size_t)160 * 1024 / (per_cu ? per_cu : 1));
@@ -1658,19 +1681,22 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
             const dim3 g((unsigned)blocks);
             auto launch = [&](auto kern, const uint8_t* a) {
                 if (shm > 64 * 1024 && (lds_rc = allow_big_lds(c, reinterpret_cast<const void*>(kern)))) return;
-                kern<<<g, kBlock, shm, c->stream>>>(p, T, a, seed, t0, d_rew, d_flags, st, tiled, ot ? *ot : no_obs);
+                kern<<<g, kBlock, shm, c->stream>>>(p, T, a, seed, t0, d_rew, d_flags, st, tiled, ot ? *ot : no_obs,
+                                                    rtr ? *rtr : no_rules);
             };
             if (d_act) {
-                if (lds_table) launch(k_rollout<W, TB, false, true, EPW, OBS>, d_act);
-                else launch(k_rollout<W, TB, false, false, EPW, OBS>, d_act);
+                if (lds_table) launch(k_rollout<W, TB, false, true, EPW, OBS, RULES>, d_act);
+                else launch(k_rollout<W, TB, false, false, EPW, OBS, RULES>, d_act);
             } else {
-                if (lds_table) launch(k_rollout<W, TB, true, true, EPW, OBS>, nullptr);
-                else launch(k_rollout<W, TB, true, false, EPW, OBS>, nullptr);
+                if (lds_table) launch(k_rollout<W, TB, true, true, EPW, OBS, RULES>, nullptr);
+                else launch(k_rollout<W, TB, true, false, EPW, OBS, RULES>, nullptr);
             }
         };
-        if (ot) go(std::integral_constant<int, 64>{}, std::true_type{});
-        else if (half) go(std::integral_constant<int, 32>{}, std::false_type{});
-        else go(std::integral_constant<int, 64>{}, std::false_type{});
+        using E64 = std::integral_constant<int, 64>;
+        if (ot) go(E64{}, std::true_type{}, std::false_type{});
+        else if (rtr) go(E64{}, std::false_type{}, std::true_type{});
+        else if (half) go(std::integral_constant<int, 32>{}, std::false_type{}, std::false_type{});
+        else go(E64{}, std::false_type{}, std::false_type{});
     });
     if (lds_rc) return lds_rc;
     return launch_check(c);
@@ -1701,6 +1727,20 @@ int sparc_rollout_obs_device(void* ctx, int32_t T, const uint8_t* d_act, uint64_
     if (!d_visited && !d_agent) return rollout_impl(c, T, d_act, seed, t0, d_rew, d_flags, d_stats, nullptr);
     const ObsTrace ot{d_visited, d_agent, (uint32_t)x_dim, (uint32_t)y_dim};
     return rollout_impl(c, T, d_act, seed, t0, d_rew, d_flags, d_stats, &ot);
+}
+
+int sparc_rollout_rules_device(void* ctx, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_t t0,
+                               int8_t* d_rew, uint8_t* d_flags, int32_t* d_stats, uint16_t* d_rule_bits) {
+    DevGuard dg;
+    Ctx* c = static_cast<Ctx*>(ctx);
+    int rc = check_ctx(c, true);
+    if (rc) return rc;
+    if (!c->rules) return fail(c, SPARC_E_STATE, "sparc_load_rules has not been called");
+    if (!d_rule_bits) return fail(c, SPARC_E_INVALID, "null rule_bits");
+    const RuleTrace rtr{RulesTab{c->r_planes, c->r_inst_range, c->r_inst, c->r_shape_range, c->r_shape_area,
+                                 c->r_shape_off, c->num_puzzles},
+                        d_rule_bits};
+    return rollout_impl(c, T, d_act, seed, t0, d_rew, d_flags, d_stats, nullptr, &rtr);
 }
 
 int sparc_step_obs_device(void* ctx, const uint8_t* d_act, int8_t* d_rew, uint8_t* d_flags, int32_t* d_visited,

@@ -62,6 +62,8 @@ _SIGS = {
                               c_int32),
     "sparc_rollout_obs_device": ([c_void_p, c_int32, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_int32, c_int32], c_int32),
+    "sparc_rollout_rules_device": ([c_void_p, c_int32, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p,
+                                    c_void_p], c_int32),
     "sparc_read_state": ([c_void_p, ctypes.POINTER(SparcStateHost)], c_int32),
     "sparc_state_ptr": ([c_void_p, c_int32, ctypes.POINTER(c_void_p)], c_int32),
     "sparc_copy_state_device": ([c_void_p, c_int32, c_void_p], c_int32),

@@ -165,6 +165,10 @@ class SparcCore:
                                                       int(t0), d_reward, d_flags, d_stats, d_visited, d_agent,
                                                       int(x_dim), int(y_dim)))
 
+    def rollout_rules_device(self, T, d_actions, d_reward, d_flags, d_stats, d_rule_bits, seed=0, t0=0):
+        self._check(self.lib.sparc_rollout_rules_device(self.ctx, int(T), d_actions, int(seed) & (2**64 - 1),
+                                                        int(t0), d_reward, d_flags, d_stats, d_rule_bits))
+
     def copy_state_device(self, which, d_out):
         self._check(self.lib.sparc_copy_state_device(self.ctx, int(which), d_out))
 

@@ -298,14 +298,17 @@ class SPaRCVecEnv:
             info["rule_bits"] = bits.clone() if self.copy else bits
         return self._step_obs_dict(bufs), reward, terminated, truncated, info
 
-    def rollout(self, T, actions=None, seed=0, t0=0, stats=None, record=True, out=None, obs=False, obs_out=None):
+    def rollout(self, T, actions=None, seed=0, t0=0, stats=None, record=True, out=None, obs=False, obs_out=None,
+                rules=False):
         """T steps of every env in ONE kernel launch.  actions: [T, N] uint8 on the GPU or None
         (counter-based random actions, sparc_rand_action(seed, env_offset + i, t0 + t)).
         Returns reward codes and flags [T, N] (int8 / uint8) if ``record`` (written into
         ``out=(reward_code, flags)`` when given).  With ``obs`` (or ``obs_out=(visited,
         agent_location)``) the 'new' observation after every step is recorded too: int32
         traces [T, N, x_dim, y_dim] under "visited" / "agent_location" (8 * x_dim * y_dim
-        bytes per env-step of HBM writes)."""
+        bytes per env-step of HBM writes).  With ``rules`` the rule audit runs after every step
+        as in the reference's step() (SPaRC_Gym.py:1227): "rule_bits" [T, N] int16 (bit k =
+        RULE_NAMES[k] passed), step t's bits equal rule_audit() after t + 1 single steps."""
         self._stream()
         n = self.num_envs
         if actions is not None:
@@ -325,6 +328,13 @@ class SPaRCVecEnv:
             raise ValueError("stats must be a contiguous int32 tensor [N, 4]")
         args = (None if actions is None else actions.data_ptr(), None if rew is None else rew.data_ptr(),
                 None if flags is None else flags.data_ptr(), None if stats is None else stats.data_ptr())
+        if rules:
+            if obs or obs_out is not None:
+                raise ValueError("rules=True records the rule bits only (no observation traces)")
+            self._load_rules()
+            bits = torch.empty((T, n), dtype=torch.int16, device=self.device)
+            self.core.rollout_rules_device(T, *args, bits.data_ptr(), seed, t0)
+            return {"reward_code": rew, "flags": flags, "rule_bits": bits}
         if not obs and obs_out is None:
             self.core.rollout_device(T, *args, seed, t0)
             return {"reward_code": rew, "flags": flags}

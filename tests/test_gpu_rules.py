@@ -119,3 +119,46 @@ def test_rules_at_scale_vs_oracle(on_gpu, sizes, full, n, max_shaped):
             checked += 1
     vec.core.sync()
     assert checked == 1200
+
+
+@pytest.mark.parametrize("sizes,max_shaped", [(((3, 3),), None), (((2, 2), (3, 3), (4, 4), (5, 5)), None),
+                                              (((7, 7), (6, 6)), 4)])
+def test_rollout_rule_bits_every_step(on_gpu, sizes, max_shaped):
+    """rollout(rules=True): the audit after every step inside the rollout launch (the reference
+    audits every step(), SPaRC_Gym.py:1227) equals step()-by-step() rule_audit() bits, and the
+    reward codes / flags equal a plain rollout's; the bits of a sample of envs and steps equal
+    the oracle's audit (oracle/rules_ref.py) of the oracle state."""
+    from sparc_gym_amd import SPaRCVecEnv, synthetic
+    from sparc_gym_amd.puzzles import process_puzzles
+    recs = synthetic.make_rule_puzzles(128, seed=3, sizes=sizes, break_prob=0.3)
+    recs += synthetic.make_puzzles(128, seed=4, sizes=sizes, full_properties=True, max_shaped=max_shaped)
+    proc = process_puzzles(recs)
+    n, T = 1024, 24
+    kw = dict(processed=proc, traceback=True, autoreset="next_step", observation="compact", rules=True,
+              max_steps=10)
+    pids = (np.arange(n) * 37) % len(proc)
+    acts = torch.randint(0, 4, (T, n), dtype=torch.uint8, device="cuda")
+    a = SPaRCVecEnv(n, **kw)
+    a.reset(options={"puzzle_index": pids})
+    ra = a.rollout(T, acts, rules=True)
+    b = SPaRCVecEnv(n, **kw)
+    b.reset(options={"puzzle_index": pids})
+    rb = b.rollout(T, acts)
+    assert torch.equal(ra["reward_code"], rb["reward_code"]) and torch.equal(ra["flags"], rb["flags"])
+    c = SPaRCVecEnv(n, **kw)
+    c.reset(options={"puzzle_index": pids})
+    bits = ra["rule_bits"].cpu().numpy()
+    refp = [dict(p) for p in proc]
+    rng = np.random.default_rng(1)
+    for t in range(T):
+        _, _, _, _, info = c.step(acts[t])
+        assert np.array_equal(bits[t], info["rule_bits"].cpu().numpy()), t
+        if t % 6 == 5:   # and a sample against the oracle's audit of the same state
+            st = c.state()
+            for i in rng.choice(n, size=50, replace=False):
+                p = refp[int(st["puzzle"][i])]
+                path = _state_points(st["visited"][:, i], c.table.pitch, p["x_size"], p["y_size"])
+                want = rules_ref.rule_bits(rules_ref.audit(p, path, (int(st["x"][i]), int(st["y"][i]))))
+                assert int(bits[t, i]) & 0x1FF == want, (t, i)
+    assert not (bits & (1 << 9)).any()   # no exact-fit search reached its node cap
+    assert len(np.unique(bits)) > 4
