@@ -200,6 +200,13 @@ int sparc_read_state(void *ctx, const sparc_state_host *out);
  * ordered on the context's stream (e.g. the per-env puzzle index after autoresets). */
 int sparc_copy_state_device(void *ctx, int32_t which, void *d_out);
 
+/* Overwrite the visited boards [words][N] (host, bit x*pitch+y) of the current state, e.g. with
+ * the planes an aliasing reference env keeps across re-loads of a puzzle (SPaRC_Gym.py:149-151:
+ * _load_puzzle binds the puzzle's planes, so a re-loaded puzzle starts with the previous
+ * episode's visited bits, which _get_legal_actions (1040) and step (1141) then read).  The
+ * start point must stay set.  Synchronous. */
+int sparc_set_visited_host(void *ctx, const uint64_t *visited);
+
 /* device pointers of the context's SoA state (zero-copy views for the host layer):
  * which: 0 visited [words][N] u64, 1 pos [N] u32 = x | y<<8 | len<<16 | off<<24,
  *        2 aux [N] u32 = trie node | outcome<<16 (1: +1, 2: -1) | pending<<18,

@@ -1935,6 +1935,16 @@ int sparc_read_state(void* ctx, const sparc_state_host* o) {
     return SPARC_OK;
 }
 
+int sparc_set_visited_host(void* ctx, const uint64_t* visited) {
+    DevGuard dg;
+    Ctx* c = static_cast<Ctx*>(ctx);
+    int rc = check_ctx(c, true);
+    if (rc) return rc;
+    if (!visited) return fail(c, SPARC_E_INVALID, "null visited");
+    HIPCHK(c, hipMemcpyAsync(c->vis, visited, sizeof(uint64_t) * c->W * c->n, hipMemcpyHostToDevice, c->stream));
+    return sparc_sync(c);
+}
+
 int sparc_state_ptr(void* ctx, int32_t which, void** d_ptr) {
     DevGuard dg;
     Ctx* c = static_cast<Ctx*>(ctx);

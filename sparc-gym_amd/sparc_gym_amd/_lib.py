@@ -66,6 +66,7 @@ _SIGS = {
                                     c_void_p], c_int32),
     "sparc_read_state": ([c_void_p, ctypes.POINTER(SparcStateHost)], c_int32),
     "sparc_state_ptr": ([c_void_p, c_int32, ctypes.POINTER(c_void_p)], c_int32),
+    "sparc_set_visited_host": ([c_void_p, c_void_p], c_int32),
     "sparc_copy_state_device": ([c_void_p, c_int32, c_void_p], c_int32),
     "sparc_load_rules": ([c_void_p, ctypes.POINTER(SparcRulesTable)], c_int32),
     "sparc_rules_device": ([c_void_p, c_void_p, c_void_p, c_void_p], c_int32),

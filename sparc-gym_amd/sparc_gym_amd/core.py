@@ -135,6 +135,13 @@ class SparcCore:
         self._check(self.lib.sparc_read_state(self.ctx, ctypes.byref(s)))
         return out
 
+    def set_visited_host(self, words):
+        """Overwrite the visited boards [words][N] uint64 of the current state."""
+        v = np.ascontiguousarray(words, np.uint64)
+        if v.shape != (self.table.words, self.num_envs):
+            raise ValueError(f"visited must have shape ({self.table.words}, {self.num_envs})")
+        self._check(self.lib.sparc_set_visited_host(self.ctx, _ptr(v)))
+
     # ---------------------------------------------------------------- device-pointer calls (async)
     def reset_device(self, d_puzzle_index, d_mask=None, d_flags=None):
         self._check(self.lib.sparc_reset_device(self.ctx, d_puzzle_index, d_mask, d_flags))

@@ -10,8 +10,14 @@ Differences (documented in DESIGN.md):
 * ``puzzles=`` accepts a local DataFrame / list of records in the SPaRC schema, because the
   hub dataset (``load_dataset``, SPaRC_Gym.py:77) needs the network; ``df_name`` etc. are
   still honoured when ``puzzles`` is None.
-* Every reset restores pristine planes (the reference's first load of a puzzle); the reference
-  aliases the planes across re-loads (SPaRC_Gym.py:149-151).
+* By default every reset restores pristine planes (the reference's first load of a puzzle).
+  The reference aliases the planes across re-loads (SPaRC_Gym.py:149-151): a puzzle loaded
+  again keeps the previous episode's ``visited`` and ``agent_location`` bits, and the stale
+  ``visited`` bits block moves (_get_legal_actions reads that plane, 1040).  ``alias_compat=True``
+  reproduces that exactly (pinned by tests/golden/alias_*.json.gz from the reference): the
+  puzzle's planes persist in ``self.puzzles``, the device board starts from them, and the
+  rule audit takes its path-based rules from the path and ``all_dots_collected`` from the
+  plane, as the reference does (400, 529).
 * ``info['rule_status']`` (the rule audit, 941-950) is computed by the k_rules kernel and laid
   out in the reference's dict shape by ``rules.rule_status``; ``rule_status=False`` skips it
   (then ``{}``).  After ``__init__`` (before any reset) it describes the loaded state with the
@@ -108,8 +114,10 @@ class SPaRC_Gym(Env):
     metadata = {"render_modes": ["human", "llm"], "render_fps": 30}
 
     def __init__(self, df_name="lkaesberg/SPaRC", df_split="all", df_set="test", render_mode=None,
-                 observation="new", traceback=False, max_steps=2000, puzzles=None, device=0, rule_status=True):
+                 observation="new", traceback=False, max_steps=2000, puzzles=None, device=0, rule_status=True,
+                 alias_compat=False):
         self.render_mode = render_mode
+        self.alias_compat = bool(alias_compat)
         self.observation = observation
         self.traceback = traceback
         self.max_steps = max_steps
@@ -137,7 +145,10 @@ class SPaRC_Gym(Env):
         self.difficulty = puzzle["difficulty"]
         self.polyshapes = puzzle["polyshapes"]
         self.x_size, self.y_size = puzzle["x_size"], puzzle["y_size"]
-        self.obs_array = OrderedDict((k, v.copy()) for k, v in puzzle["obs_array"].items())
+        if self.alias_compat:   # the puzzle's own planes, aliased across re-loads (149-151)
+            self.obs_array = puzzle["obs_array"]
+        else:
+            self.obs_array = OrderedDict((k, v.copy()) for k, v in puzzle["obs_array"].items())
         self.color_array = puzzle["color_array"]
         self.additional_info = puzzle["additional_info"]
         if self.observation == "SPaRC":                                              # 153-164
@@ -155,7 +166,18 @@ class SPaRC_Gym(Env):
 
         flags = self._core.reset_host(np.array([index], np.uint32))
         self._legal = int(flags[0] >> 2) & 0xF
-        self._sync_planes()
+        if self.alias_compat:
+            sx, sy = int(self.start_location[0]), int(self.start_location[1])
+            vis = self.obs_array["visited"]
+            vis[sx, sy] = 1                                                          # 185
+            self._core.set_visited_host(self._plane_words(vis))
+            self._legal = self._start_legal_mask()
+            self.obs_array["agent_location"][sx, sy] = 1                             # 186
+            st = self._core.read_state()
+            self.current_step = int(st["step"][0])
+            self.outcome_reward = int(st["outcome"][0])
+        else:
+            self._sync_planes()
         self.obs_array["target_location"][self._target_location[0], self._target_location[1]] = 1
 
         if self.observation == "new":                                                # 190-196
@@ -176,8 +198,10 @@ class SPaRC_Gym(Env):
         self._action_to_direction = {0: np.array([1, 0]), 1: np.array([0, -1]),
                                      2: np.array([-1, 0]), 3: np.array([0, 1])}
 
-    def _sync_planes(self):
-        """Mirror visited / agent_location planes from the device state."""
+    def _sync_planes(self, old=None):
+        """Mirror visited / agent_location planes from the device state.  alias_compat: the
+        agent plane is edited as the reference edits it (the point left -> 0, the new point
+        -> 1, 1145-1157 / 1170-1179), so stale bits of an earlier episode stay."""
         st = self._core.read_state()
         X, Y, pitch = self.x_size, self.y_size, self._core.table.pitch
         bits = st["visited"][:, 0]
@@ -186,12 +210,36 @@ class SPaRC_Gym(Env):
         vis = ((bits[(b >> np.uint64(6)).astype(np.int64)] >> (b & np.uint64(63))) & np.uint64(1)).astype(np.int32)
         self.obs_array["visited"][...] = vis
         agent = self.obs_array["agent_location"]
-        agent[...] = 0
         x, y = int(st["x"][0]), int(st["y"][0])
+        if not self.alias_compat:
+            agent[...] = 0
+        elif old is not None and old != (x, y):
+            agent[old[0], old[1]] = 0
         agent[x, y] = 1
         self.current_step = int(st["step"][0])
         self.outcome_reward = int(st["outcome"][0])
         return x, y, int(st["path_len"][0])
+
+    def _plane_words(self, plane):
+        """[X][Y] 0/1 plane -> the device's visited board [words][1] (bit x * pitch + y)."""
+        W, pitch = self._core.table.words, self._core.table.pitch
+        words = np.zeros((W, 1), np.uint64)
+        for x, y in zip(*np.nonzero(np.asarray(plane))):
+            b = int(x) * pitch + int(y)
+            words[b >> 6, 0] |= np.uint64(1) << np.uint64(b & 63)
+        return words
+
+    def _start_legal_mask(self):
+        """_get_legal_actions (1024-1051) at a fresh start (path of one point): in bounds, not a
+        gap, not visited (the aliased plane may hold stale bits)."""
+        m = 0
+        sx, sy = int(self.start_location[0]), int(self.start_location[1])
+        for a, (dx, dy) in enumerate(((1, 0), (0, -1), (-1, 0), (0, 1))):
+            nx, ny = sx + dx, sy + dy
+            if 0 <= nx < self.x_size and 0 <= ny < self.y_size and self.obs_array["gaps"][nx, ny] == 0 \
+                    and self.obs_array["visited"][nx, ny] == 0:
+                m |= 1 << a
+        return m
 
     # ------------------------------------------------------------------ gym API
     def reset(self, seed=None, options=None):
@@ -215,7 +263,7 @@ class SPaRC_Gym(Env):
         """SPaRC_Gym.py:1111-1238; the transition runs in the HIP step kernel."""
         codes, flags = self._core.step_host(np.array([action_code(action)], np.uint8))
         old = (int(self._agent_location[0]), int(self._agent_location[1]))
-        x, y, plen = self._sync_planes()
+        x, y, plen = self._sync_planes(old)
         if (x, y) != old:
             if plen < len(self.path):                                                # traceback pop
                 if self.observation == "SPaRC":
@@ -250,6 +298,23 @@ class SPaRC_Gym(Env):
             self.rule_status = {}
             return self.rule_status
         r = self._core.rules_host(region=True, fit=True)
+        if self.alias_compat:
+            # the path-based rules and the regions read self.path (400, 503-515, 639), the dots
+            # rule the visited plane (529): with stale plane bits the audit runs on the path's
+            # points, and the dots bit comes from the audit of the plane
+            path_plane = np.zeros_like(self.obs_array["visited"])
+            for px, py in self.path:
+                path_plane[px, py] = 1
+            if (path_plane != self.obs_array["visited"]).any():
+                self._core.set_visited_host(self._plane_words(path_plane))
+                rp = self._core.rules_host(region=True, fit=True)
+                self._core.set_visited_host(self._plane_words(self.obs_array["visited"]))
+                dots = 1 << 3   # all_dots_collected (RULE_NAMES order)
+                bits = (int(rp["bits"][0]) & ~dots & ~(1 << 8)) | (int(r["bits"][0]) & dots)
+                if (bits & 0xFF) == 0xFF:
+                    bits |= 1 << 8   # all_rules_satisfied: every core rule (931-934)
+                rp["bits"][0] = bits
+                r = rp
         rmap = region_map_of(r["region"][0], self.x_size, self.y_size, self._core.table.pitch)
         self.rule_status = _rule_status(self.puzzles[self.current_puzzle_index], self.obs_array, self.path,
                                         self._agent_location, self._target_location, r["bits"][0], rmap,

@@ -46,3 +46,14 @@ def test_seeded_reset_index_matches_reference():
     for seed, idx in r["seeded"]:
         Env.reset(env, seed=seed)
         assert int(env.np_random.integers(r["n"])) == idx, seed
+
+
+def test_alias_fixtures_hold_stale_resets():
+    """The aliasing fixtures (make_alias_golden.py) re-load puzzles in one reference env: most
+    resets start with the previous episode's visited bits (more than the start point), and some
+    start with fewer legal moves than a fresh load would give."""
+    from golden_io import load
+    for name in ("alias_tb1", "alias_tb0", "alias_rules", "alias_mixed"):
+        g = load(name)
+        stale = sum(len(ep["reset"]["visited"]["nz"]) > 1 for ep in g["episodes"])
+        assert stale >= len(g["episodes"]) // 2, name
