@@ -11,6 +11,9 @@
   size-independent invariants on the GPU: the agent plane is one-hot and inside the visited
   plane, nothing lies outside the env's own lattice, the visited count moves by one per
   moving step and restarts at 1 on a reset step, and at the end it equals path_len.
+* c4c: the same 262,144-env mixed pool without planes, through the multi-word split kernel
+  (k_rolloutWs), 256 steps with autoresets: sampled oracle columns (reward codes, flags, final
+  state, stats) and, for every env, the stats against the output traces.
 """
 import numpy as np
 import pytest
@@ -147,3 +150,44 @@ def test_c4_262144_envs_new_planes_sampled_oracle_and_invariants(on_gpu):
     s = v.state()
     assert np.array_equal(cnt[-1].cpu().numpy(), s["path_len"].astype(np.int64))
     assert np.array_equal(pid_t[-1].cpu().numpy(), s["puzzle"].astype(np.int64))
+
+
+def test_c4c_262144_envs_split_kernel_sampled_oracle(on_gpu):
+    from sparc_gym_amd import SPaRCVecEnv
+    from sparc_gym_amd.core import visited_planes
+    proc, table = _bench_pool(((2, 2), (3, 3), (4, 4), (5, 5)), True)
+    n, T, ms = 262144, 256, 60                    # max_steps 60: many autoresets inside the launch
+    pids = _bench_pids(n)
+    v = SPaRCVecEnv(n, processed=proc, table=table, traceback=True, max_steps=ms, observation="compact")
+    v.reset(options={"puzzle_index": pids})
+    assert table.words == 2
+    g = torch.Generator(device="cuda")
+    g.manual_seed(11)
+    acts = torch.randint(0, 4, (T, n), dtype=torch.uint8, device="cuda", generator=g)
+    stats = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
+    out = v.rollout(T, acts, stats=stats)
+    r, f = out["reward_code"], out["flags"]
+    # every env: the stats are the sums of its own trace
+    st = stats.cpu().numpy()
+    assert np.array_equal(st[:, 0], r.to(torch.int64).sum(0).cpu().numpy())
+    assert np.array_equal(st[:, 1], ((f & 3) != 0).sum(0).cpu().numpy())
+    assert np.array_equal(st[:, 2], (((f & 3) != 0) & (r == 100)).sum(0).cpu().numpy())
+    assert np.array_equal(st[:, 3], ((f & 64) != 0).sum(0).cpu().numpy())
+    assert not bool(((f & 3) == 3).any())
+    # sampled oracle columns, the first and last envs included (large-offset indexing)
+    rng = np.random.default_rng(1)
+    idx = np.unique(np.concatenate([rng.choice(n, 2000, replace=False), np.arange(n - 256, n), np.arange(256)]))
+    ti = torch.from_numpy(idx).cuda()
+    o = COracle(_oracle_pool(proc), len(idx), True, ms, autoreset=1)
+    o.reset(pids[idx])
+    ost = np.zeros((len(idx), 4), np.int32)
+    ro, fo = o.rollout(T, np.ascontiguousarray(acts[:, ti].cpu().numpy()), stats=ost)
+    assert np.array_equal(r[:, ti].cpu().numpy(), ro)
+    assert np.array_equal(f[:, ti].cpu().numpy(), fo)
+    assert np.array_equal(st[idx], ost)
+    assert (fo & 64).sum() > len(idx)
+    s, so = v.state(), o.state()
+    for k, ko in (("x", "x"), ("y", "y"), ("step", "step"), ("path_len", "path_len"), ("puzzle", "pid"),
+                  ("outcome", "outcome")):
+        assert np.array_equal(s[k][idx], so[ko]), k
+    assert np.array_equal(visited_planes(s["visited"][:, idx], table, 16, 16), so["visited"].astype(np.int32))
