@@ -46,6 +46,8 @@ def test_null_context_is_an_error_not_a_crash():
     assert lib.sparc_step_obs_device(None, None, None, None, None, None, 7, 7, None, None) != 0
     assert lib.sparc_rollout_obs_device(None, 4, None, 0, 0, None, None, None, None, None, 7, 7) != 0
     assert lib.sparc_rollout_device(None, 4, None, 0, 0, None, None, None) != 0
+    assert lib.sparc_rollout_rules_device(None, 4, None, 0, 0, None, None, None, None) != 0
+    assert lib.sparc_set_visited_host(None, None) != 0
     assert lib.sparc_sync(None) != 0
     assert lib.sparc_destroy(None) == 0
 
