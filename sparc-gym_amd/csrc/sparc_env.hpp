@@ -648,6 +648,78 @@ struct Env<1, TB, Stack> {
         return done ? c_done : c_move;
     }
 
+    // ---- k_rollout1s move wave: phase_move with the split kernel's conventions (the rest of
+    // the state as phase_move):
+    //   * actions arrive sanitised to 0..4 (the I/O wave maps every byte >= 4 to 4, which reads
+    //     legal bit 4 = 0: never legal);
+    //   * with traceback the move stack is addressed through sp = this lane's slot len-1 (an
+    //     LDS byte address stepping 64 per move), and the traceback bias is folded into it:
+    //     (sp + bks) >> 31 is the len >= 3 or (len == 2, open start) test of legal_mask, so
+    //     len is not kept in the loop (the caller derives it from sp before store);
+    //   * it returns the hand-over word (flag byte | (fwd - pop) << 8) directly.
+    uint32_t sp = 0, bks = 0;   // sp: 32-bit LDS address
+    typedef __attribute__((address_space(3))) uint8_t lds_u8;
+    __device__ __forceinline__ static lds_u8* lds_byte(uint32_t a) { return (lds_u8*)(uintptr_t)a; }
+    __device__ __forceinline__ static uint32_t lds_addr(const uint8_t* g) { return (uint32_t)(uintptr_t)(lds_u8*)g; }
+    __device__ __forceinline__ void sp_from_len(uint32_t col_addr) {
+        sp = col_addr + (len - 1u) * 64u;
+        bks = 0x80000000u - col_addr - 128u + 64u * ((~pflags >> 2) & 1u);
+    }
+    __device__ __forceinline__ uint32_t legal_mask_s(uint32_t P) {
+        w = (uint32_t)(fr >> (e & 63u));
+        const uint32_t ud = __builtin_amdgcn_ubfe(w, P - 2u, 4u);
+        uint32_t m = (ud & 10u) | (((w << 2) & 4u) | __builtin_amdgcn_ubfe(w, 2u * P, 1u));
+        if constexpr (TB) m |= ((sp + bks) >> 31) << rl;
+        return m;
+    }
+    __device__ __forceinline__ void reset_next_s(const Params& p, const uint4* mrow, uint32_t col_addr) {
+        if (pending & (uint32_t)(p.autoreset == 1)) {
+            e = rrow & 0xFFu;
+            tgt = (rrow >> 8) & 0xFFu;
+            pflags = rrow >> 16;
+            fr = rinit;
+            sp = col_addr;                         // len = 1
+            len = 1;
+            bks = 0x80000000u - col_addr - 128u + 64u * ((~pflags >> 2) & 1u);
+            step = -1;   // this step's increment brings it to 0
+            rs = 1;
+            prefetch_reset_m(mrow, rpid);
+        }
+    }
+    __device__ __forceinline__ uint32_t phase_move_s(const Params& p, uint32_t a) {
+        const uint32_t P = p.pitch;
+        step = __builtin_elementwise_add_sat(step, 1);                              // 1132
+        const bool trunc0 = step >= p.max_steps;                                    // 1134
+        const uint32_t moved = (legal >> a) & (rs ^ 1u) & 1u;                       // 1137
+        const uint32_t pos = __builtin_amdgcn_ubfe(p.nbr_pos, a << 3, 8u);
+        const uint32_t pop = TB ? moved & ~__builtin_amdgcn_ubfe(w, pos, 1u) : 0u;  // 1141-1166
+        const uint32_t fwd = moved ^ pop;                                            // 1167-1188
+        const int32_t d = (int32_t)pos - (int32_t)P;
+        const uint32_t tog = e + (fwd ? pos : P);
+        fr ^= (uint64_t)moved << (tog & 63u);
+        const int32_t dl = (int32_t)fwd - (int32_t)pop;
+        if constexpr (TB) {
+            const uint32_t ar = a ^ 2u;
+            *lds_byte(sp) = (uint8_t)ar;             // slot len-1
+            rl = fwd ? ar : (pop ? pnr : rl);
+            sp = (uint32_t)((int32_t)sp + __mul24(dl, 64));
+        } else {
+            len += fwd;   // no pops without traceback
+        }
+        e = (uint32_t)((int32_t)e + __mul24((int32_t)moved, d));
+        legal = legal_mask_s(P);
+        const uint32_t live = rs ^ 1u;
+        const uint32_t term = e == tgt ? live : 0u;                                  // 1192
+        const uint32_t trunc = (trunc0 | (legal == 0)) ? live ^ term : 0u;          // 1195-1199
+        pending = term | trunc;
+        // the move before the last (slot len-3 after the step; a harmless read of the slots
+        // below the stack when len < 3, where the traceback rule is off)
+        if constexpr (TB) pnr = *lds_byte(sp - 128u);
+        const uint32_t hw = (uint32_t)(dl << 8) | (rs << 6) | (legal << 2) | (trunc << 1) | term;
+        rs = 0;
+        return hw;
+    }
+
     // one whole step (k_step, and the generic-width interface)
     template <class Src>
     __device__ __forceinline__ int advance(const Params& p, const Src& src, uint32_t a, uint32_t& flags) {

@@ -636,6 +636,15 @@ constexpr size_t kS_Base = kS_Fin + 4 * 64 * 2 * sizeof(uint4);
 // LDS bytes of the staged rows: move rows + trie rows, 16 B each per puzzle
 __host__ __device__ constexpr size_t split_table_bytes(uint32_t P) { return (size_t)P * 2 * sizeof(uint4); }
 
+// four action bytes with every byte >= 4 mapped to 4 (never legal: legal bit 4 is 0), so the
+// move wave tests legality with one shift
+__device__ __forceinline__ uint32_t clamp_actions4(uint32_t x) {
+    const uint32_t t = x & 0xFCFCFCFCu;                                   // bits that make a byte >= 4
+    const uint32_t nz = (((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;   // 0x80: byte >= 4
+    const uint32_t bm = (nz >> 7) * 0xFFu;                               // 0xFF in those bytes
+    return (x & ~bm) | (bm & 0x04040404u);
+}
+
 // the flag bytes (byte 0) of four hand-over words
 __device__ __forceinline__ uint32_t flag_bytes4(const u32x4 w) {
     const uint32_t lo = __builtin_amdgcn_perm(w.y, w.x, 0x0C0C0400u);
@@ -676,7 +685,11 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         const uint32_t r = lane >> 2, c = (lane & 3u) * 16u;
         auto load_tile = [&](int32_t k) {                        // actions of tile k -> buffer k % 3
             if constexpr (!RAND) {
-                const u32x4 v = nt_load16(act + (size_t)(k * kTile + r) * n + wg_base + io * 64 + c);
+                u32x4 v = nt_load16(act + (size_t)(k * kTile + r) * n + wg_base + io * 64 + c);
+                v.x = clamp_actions4(v.x);
+                v.y = clamp_actions4(v.y);
+                v.z = clamp_actions4(v.z);
+                v.w = clamp_actions4(v.w);
                 *reinterpret_cast<u32x4*>(smem + io * kS_Pair + kS_Act + (k % 3) * (kTile * 64) + r * 64 + c) = v;
             }
         };
@@ -723,6 +736,8 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         const uint32_t pend0 = e.pending;
         const uint64_t gid = p.env_offset + i;
         uint32_t* th = reinterpret_cast<uint32_t*>(pb + kS_FH) + lane;
+        const uint32_t col_addr = e.lds_addr(pb + kS_Stk + lane);
+        e.sp_from_len(col_addr);
         __syncthreads();                                         // B_0
         for (int32_t k = 0; k < K; ++k) {
             // tile k's actions (buffer k % 3; the trie wave reads them one tile later)
@@ -742,9 +757,8 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const uint32_t row = (uint32_t)(k * kTile + g + j) & (kRing - 1);
-                    e.reset_next_m(p, mrow);
-                    const uint32_t f = e.phase_move(p, av[j]);
-                    th[row * 64] = hand_word32(e.s_fwd, e.s_pop, f);
+                    e.reset_next_s(p, mrow, col_addr);
+                    th[row * 64] = e.phase_move_s(p, av[j]);
                 }
             }
             __syncthreads();                                     // B_{k+1}
@@ -757,6 +771,7 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         e.off = fs.x >> 16;
         e.outcome = e.pending ? (fs.y == 0u ? 1u : 2u) : 0u;   // outcome_reward after the last step
         e.pid = fc.y;
+        if constexpr (TB) e.len = (e.sp - col_addr) / 64u + 1u;
         e.store(p, src, i);
         if (stats) {
             // autoresets: one per done step before the last, plus one for a done step carried in
