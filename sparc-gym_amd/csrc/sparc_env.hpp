@@ -695,7 +695,9 @@ struct Env<1, TB, Stack> {
         const uint32_t pop = TB ? moved & ~__builtin_amdgcn_ubfe(w, pos, 1u) : 0u;  // 1141-1166
         const uint32_t fwd = moved ^ pop;                                            // 1167-1188
         const int32_t d = (int32_t)pos - (int32_t)P;
-        const uint32_t tog = e + (fwd ? pos : P);
+        // free board: a forward move takes the target (bit e + P + d), a pop frees the point
+        // it leaves (bit e + P)
+        const uint32_t tog = (uint32_t)((int32_t)e + __mul24((int32_t)fwd, d)) + P;
         fr ^= (uint64_t)moved << (tog & 63u);
         const int32_t dl = (int32_t)fwd - (int32_t)pop;
         if constexpr (TB) {
@@ -709,13 +711,15 @@ struct Env<1, TB, Stack> {
         e = (uint32_t)((int32_t)e + __mul24((int32_t)moved, d));
         legal = legal_mask_s(P);
         const uint32_t live = rs ^ 1u;
-        const uint32_t term = e == tgt ? live : 0u;                                  // 1192
-        const uint32_t trunc = (trunc0 | (legal == 0)) ? live ^ term : 0u;          // 1195-1199
-        pending = term | trunc;
+        const bool at_tgt = e == tgt;                                                // 1192
+        const uint32_t term = at_tgt ? live : 0u;
+        const uint32_t done = (trunc0 | (legal == 0) | at_tgt) ? live : 0u;        // 1195-1199
+        pending = done;
         // the move before the last (slot len-3 after the step; a harmless read of the slots
         // below the stack when len < 3, where the traceback rule is off)
         if constexpr (TB) pnr = *lds_byte(sp - 128u);
-        const uint32_t hw = (uint32_t)(dl << 8) | (rs << 6) | (legal << 2) | (trunc << 1) | term;
+        // flag bits: term | trunc << 1 = 2 * done - term (trunc = done and not term)
+        const uint32_t hw = (uint32_t)(dl << 8) | (rs << 6) | (legal << 2) | (2u * done - term);
         rs = 0;
         return hw;
     }
