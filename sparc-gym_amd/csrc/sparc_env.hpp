@@ -656,7 +656,7 @@ struct Env<1, TB, Stack> {
     //     LDS byte address stepping 64 per move), and the traceback bias is folded into it:
     //     (sp + bks) >> 31 is the len >= 3 or (len == 2, open start) test of legal_mask, so
     //     len is not kept in the loop (the caller derives it from sp before store);
-    //   * it returns the hand-over word (flag byte | (fwd - pop) << 8) directly.
+    //   * it returns the hand-over word (flag byte | (fwd - pop) << 16) directly.
     uint32_t sp = 0, bks = 0;   // sp: 32-bit LDS address
     typedef __attribute__((address_space(3))) uint8_t lds_u8;
     __device__ __forceinline__ static lds_u8* lds_byte(uint32_t a) { return (lds_u8*)(uintptr_t)a; }
@@ -719,7 +719,7 @@ struct Env<1, TB, Stack> {
         // below the stack when len < 3, where the traceback rule is off)
         if constexpr (TB) pnr = *lds_byte(sp - 128u);
         // flag bits: term | trunc << 1 = 2 * done - term (trunc = done and not term)
-        const uint32_t hw = (uint32_t)(dl << 8) | (rs << 6) | (legal << 2) | (2u * done - term);
+        const uint32_t hw = (uint32_t)(dl << 16) | (rs << 6) | (legal << 2) | (2u * done - term);
         rs = 0;
         return hw;
     }

@@ -40,12 +40,12 @@ struct SplitGeom {
 
 // 16-bit hand-over word of the multi-word kernel: bits 0-7 the flag byte, bits 8-9
 // fwd - pop + 1, bits 10-11 action & 3.  The trie wave widens it to TrieLane's word (flag byte
-// | (fwd - pop) << 8) and the action.
+// | (fwd - pop) << 16) and the action.
 __device__ __forceinline__ uint32_t hand_word16(uint32_t a, uint32_t fwd, uint32_t pop, uint32_t f) {
     return f | ((fwd + 1u - pop) << 8) | ((a & 3u) << 10);
 }
 __device__ __forceinline__ uint32_t widen_hand_word(uint32_t h) {
-    return (h & 0xFFu) | ((__builtin_amdgcn_ubfe(h, 8u, 2u) - 1u) << 8);
+    return (h & 0xFFu) | ((__builtin_amdgcn_ubfe(h, 8u, 2u) - 1u) << 16);
 }
 
 template <bool TB>

@@ -7,7 +7,8 @@
 // step's action (which the trie wave reads from the action tile itself):
 //
 //   bits  0-7   the flag byte   term | trunc << 1 | legal << 2 | autoreset << 6
-//   bits  8-31  fwd - pop       (+1 forward move, -1 traceback pop, 0 no move), two's complement
+//   bits 16-31  fwd - pop       (+1 forward move, -1 traceback pop, 0 no move), 16-bit two's
+//                               complement (bit 16 = moved)
 //
 // so the move wave packs two fields (the flag byte it outputs anyway, and the move).
 //
@@ -40,7 +41,7 @@ struct TrieLane {
     int32_t Oneg = -100;
     uint32_t rx = ~0u, ry = ~0u;   // record of the current node (S & 0x7FFF)
     uint32_t base = 0, tmax = 0;
-    int32_t hs = 0;                 // the puzzle has solutions (the +-1 rewards apply, 1217)
+    int32_t hs = 0, hsn = 0;        // the puzzle has solutions (the +-1 rewards apply, 1217); -hs
     uint32_t pid = 0, npid = 0;
     uint4 nx;                       // trie row of npid, read at the previous reset
     int acc_x = 0;                  // sum of reward codes
@@ -60,6 +61,7 @@ struct TrieLane {
         base = r.z;
         tmax = r.w >> 17;
         hs = (int32_t)((r.w >> 14) & 1u);
+        hsn = -hs;
         S = ((ps >> 24) << 16) | (ax & 0x7FFFu) | (((ax >> 19) & 1u) << 15);
         Oneg = ((ax >> 16) & 3u) == 1u ? 0 : -100;
         if ((r.w & 0x10000u) == 0u) {   // rootless puzzles keep off >= 1: the record is never read
@@ -84,6 +86,7 @@ struct TrieLane {
             base = nx.z;
             S = nx.w & 0x18000u;
             hs = (int32_t)((nx.w >> 14) & 1u);
+            hsn = -hs;
             tmax = nx.w >> 17;
         }
         // the row of the next reset, read every step outside the branch: read inside it, the
@@ -94,15 +97,15 @@ struct TrieLane {
         // decides; off the trie (or without a child) the move counts the depth instead.
         const uint64_t xy = ((uint64_t)ry << 32) | rx;
         const uint32_t c = (uint32_t)(xy >> ((a << 4) & 0x30u));
-        const uint32_t dd = (hw << 8) & 0xFFFF0000u;           // (fwd - pop) << 16; bit 16: moved
+        const uint32_t dd = hw & 0xFFFF0000u;                  // (fwd - pop) << 16; bit 16: moved
         const uint32_t key = __builtin_amdgcn_ubfe(c, 0u, 16u) | (S & 0xFFFF0000u) | (~dd & 0x10000u);
         const bool take = key < 0xFFFFu;
         S = take ? key : S + dd;
         // the record changes only with the node (exec-masked gather; a random walk is off the
-        // trie on most steps)
+        // trie on most steps).  Every field of a record holds a node of the same puzzle
+        // (validated by sparc_load_puzzles), so no clamp here; load() clamps the stored node.
         if (take) {
-            const uint32_t node = S & 0x7FFFu;
-            const uint2 rec = trie8[base + (node < tmax ? node : tmax)];
+            const uint2 rec = trie8[base + (S & 0x7FFFu)];
             rx = rec.x;
             ry = rec.y;
         }
@@ -111,7 +114,7 @@ struct TrieLane {
         // nor is done)
         const uint32_t x = S >> 15;                            // 0 on, 1 on a solution, >= 2 off
         const int cd = x == 1u ? 100 : Oneg;
-        const int cm = hw >= 0x100u ? (x < 2u ? hs : -hs) : 0;
+        const int cm = hw >= 0x10000u ? (x < 2u ? hs : hsn) : 0;
         const bool done = (hw & 3u) != 0u;
         const int code = done ? cd : cm;
         Oneg = done ? (cd < 0 ? cd : 0) : -100;
@@ -124,7 +127,7 @@ struct TrieLane {
 
 // the move wave's side of the hand-over word (see above)
 __device__ __forceinline__ uint32_t hand_word32(uint32_t fwd, uint32_t pop, uint32_t f) {
-    return ((fwd - pop) << 8) | f;
+    return ((fwd - pop) << 16) | f;
 }
 
 }  // namespace sparc
