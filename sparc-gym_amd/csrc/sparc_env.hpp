@@ -697,7 +697,11 @@ struct Env<1, TB, Stack> {
         const int32_t d = (int32_t)pos - (int32_t)P;
         // free board: a forward move takes the target (bit e + P + d), a pop frees the point
         // it leaves (bit e + P)
-        const uint32_t tog = (uint32_t)((int32_t)e + __mul24((int32_t)fwd, d)) + P;
+        // only tog & 63 is used, so fwd * d may be taken mod 2^24: one full-rate v_mad_u32_u24
+        // (written out: the compiler selects fwd * d, in any spelling, as the quarter-rate
+        // v_mul_lo_u32)
+        uint32_t tog;
+        asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(tog) : "v"(fwd), "v"(d), "v"(e + P));
         fr ^= (uint64_t)moved << (tog & 63u);
         const int32_t dl = (int32_t)fwd - (int32_t)pop;
         if constexpr (TB) {
