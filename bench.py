@@ -40,8 +40,15 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level par
 # VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles per SIMD
 # (MI355X_MICROARCH.md, Wave scheduling), at the 2.4 GHz peak engine clock
 VALU_PEAK_WAVE_INSTS = 1024 * 2.4e9 / 2
-CSRC_FILES = ("sparc-gym_amd/csrc/sparc_kernels.hip", "sparc-gym_amd/csrc/sparc_env.hpp",
-              "sparc-gym_amd/csrc/sparc_rules.hpp", "sparc-gym_amd/csrc/sparc_trie.hpp", "include/sparc_gym_amd.h", "sparc-gym_amd/Makefile")
+
+
+def csrc_files():
+    """Every kernel source (all of csrc/, so a new header can never be left out), the ABI
+    header and the Makefile, repo-relative and sorted."""
+    import glob
+    srcs = sorted(os.path.relpath(f, REPO) for f in glob.glob(os.path.join(REPO, "sparc-gym_amd", "csrc", "*"))
+                  if f.endswith((".hip", ".hpp", ".h", ".cpp")))
+    return tuple(srcs) + ("include/sparc_gym_amd.h", "sparc-gym_amd/Makefile")
 
 CONFIGS = {
     # name: (grid sizes, full property set, traceback, 'new' observation planes every step)
@@ -156,7 +163,7 @@ def csrc_hash():
     counter summary belongs to."""
     import hashlib
     h = hashlib.sha256()
-    for f in CSRC_FILES:
+    for f in csrc_files():
         h.update(f.encode())
         h.update(open(os.path.join(REPO, f), "rb").read())
     return h.hexdigest()[:16]
@@ -209,8 +216,58 @@ def physical_cores():
     return len(phys) or None, logical or os.cpu_count(), aff, quota
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv, extra_env=None, poll_s=0.2):
+    """Start n rank processes of ``argv`` (one per GPU: LOCAL_RANK = RANK = r, WORLD_SIZE = n,
+    rendezvous on 127.0.0.1) as children of a parent that never touches the GPU, and wait for
+    them.  Returns the exit code: 0 when every rank succeeded, else the first failing rank's code
+    (the other ranks are then terminated by PID, so none is left waiting in a collective)."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GROUP_RANK="0")
+        env.update(extra_env or {})
+        procs.append(subprocess.Popen(argv, env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        time.sleep(poll_s)
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in live:
+                    q.terminate()
+    for p in procs:
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+    return rc
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N` (no torchrun): one rank process per GPU, started before
+        # this process imports torch or makes any GPU call
+        return launch_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                            {"SPARC_BENCH_LAUNCHER": "1"})
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world_env}: the job would not measure "
+                         f"{args.gpus} GPUs")
     import torch
     import torch.distributed as dist
     from sparc_gym_amd import SPaRCVecEnv, synthetic
@@ -226,6 +283,13 @@ def main():
     local = local_env % max(1, ndev)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    # which physical GPU each rank drives (PCI domain / bus / device): distinct unless rehearsing
+    props = torch.cuda.get_device_properties(dev)
+    ident = sdist.gather_values([rank, local, props.pci_domain_id, props.pci_bus_id, props.pci_device_id], dev)
+    pci = [tuple(int(v) for v in r[2:]) for r in ident]
+    if world != args.gpus or (len(set(pci)) != len(pci) and not args.rehearsal):
+        raise SystemExit(f"rank {rank}: world {world} (asked {args.gpus}), GPUs per rank {pci}: need one "
+                         f"distinct GPU per rank (--rehearsal lets ranks share GPUs, for tests only)")
 
     sizes, full, tb, obs = CONFIGS[args.config]
     if args.envs <= 0:
@@ -307,6 +371,7 @@ def main():
     kern_ms = [a.elapsed_time(b) for (a, b), _ in events]
     steps_per_launch = [c for _, c in events]
     avg_ms = float(np.mean(kern_ms))
+    rank_ms = sdist.gather_values([avg_ms, t1 - t0], dev)   # per rank: kernel ms, wall s
     avg_T = float(np.mean(steps_per_launch))
     value = world * n * T * K / elapsed
     # algorithmic HBM bytes per launch: per env-step action 1 + reward 1 + flags 1; per env and
@@ -348,7 +413,14 @@ def main():
         "unit": "env-steps/s",
         "n_gpus": world,
         "world_observed": {"world_size": observed_world, "backend": backend, "gpus_visible": ndev,
-                           "rehearsal": bool(args.rehearsal)},
+                           "rehearsal": bool(args.rehearsal),
+                           "distinct_gpus": len(set(pci)),
+                           "rank_gpu_pci": [list(p) for p in pci],
+                           "per_rank_kernel_ms": [round(r[0], 4) for r in rank_ms],
+                           "per_rank_wall_s": [round(r[1], 6) for r in rank_ms],
+                           "launcher": ("bench.py (child per rank)" if os.environ.get("SPARC_BENCH_LAUNCHER")
+                                        else "torchrun" if "TORCHELASTIC_RUN_ID" in os.environ
+                                        else "external" if world > 1 else "none")},
         "steps": K,
         "warmup": W,
         "ms_per_step": round(elapsed * 1e3 / K, 6),   # per bench step: T env-steps of every env
@@ -394,4 +466,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -47,7 +47,8 @@ enum {
     SPARC_E_INVALID = -1,   /* bad argument / shape / puzzle index              */
     SPARC_E_HIP = -2,       /* HIP runtime error                                  */
     SPARC_E_STATE = -3,     /* call order (e.g. step before load_puzzles/reset)   */
-    SPARC_E_NOMEM = -4
+    SPARC_E_NOMEM = -4,
+    SPARC_E_COMM = -5       /* RCCL unavailable or a collective failed            */
 };
 
 enum { SPARC_AUTORESET_NONE = 0, SPARC_AUTORESET_NEXT_STEP = 1 };
@@ -203,8 +204,9 @@ int sparc_copy_state_device(void *ctx, int32_t which, void *d_out);
 /* Overwrite the visited boards [words][N] (host, bit x*pitch+y) of the current state, e.g. with
  * the planes an aliasing reference env keeps across re-loads of a puzzle (SPaRC_Gym.py:149-151:
  * _load_puzzle binds the puzzle's planes, so a re-loaded puzzle starts with the previous
- * episode's visited bits, which _get_legal_actions (1040) and step (1141) then read).  The
- * start point must stay set.  Synchronous. */
+ * episode's visited bits, which _get_legal_actions (1040) and step (1141) then read).  Every
+ * env's board must hold its start point (visited[start] = 1, SPaRC_Gym.py:185) and no bit
+ * outside its puzzle's lattice, else SPARC_E_INVALID and the state is unchanged.  Synchronous. */
 int sparc_set_visited_host(void *ctx, const uint64_t *visited);
 
 /* device pointers of the context's SoA state (zero-copy views for the host layer):
@@ -266,6 +268,25 @@ int sparc_load_rules(void *ctx, const sparc_rules_table *table);
  * check and the exact fit).  Device pointers; any output may be NULL. */
 int sparc_rules_device(void *ctx, uint16_t *d_bits, uint8_t *d_region, uint64_t *d_fit);
 int sparc_rules_host(void *ctx, uint16_t *bits, uint8_t *region, uint64_t *fit);
+
+/* ---- multi-GPU: the end-of-batch gather over RCCL (xGMI) -------------------------------------
+ * The envs shard across GPUs as contiguous global id ranges (env_offset), one process and one
+ * context per GPU, no data-path collective; after a rollout batch the per-env stats are gathered
+ * with ONE ncclAllGather (SURVEY.md §8b/§8e "sparc_rccl_gather").  The reference has no
+ * counterpart: it is one env per process (SPaRC_Gym.py:44; llm_host.py:257-264 runs independent
+ * envs concurrently).  librccl is opened on first use (SPARC_E_COMM when absent).
+ *  sparc_comm_unique_id  rank 0 creates the rendezvous id (ncclGetUniqueId) and hands the
+ *                        SPARC_COMM_ID_BYTES bytes to every rank over any channel it has;
+ *  sparc_comm_init       every rank joins (ncclCommInitRank on the context's GPU; blocks until
+ *                        all nranks have joined);
+ *  sparc_gather_stats    d_stats [N][4] int32 of this rank (sparc_rollout_device's) ->
+ *                        d_out [nranks][N][4] on every rank, ordered by rank = by global env id;
+ *                        asynchronous on the context's stream, N equal on every rank. */
+#define SPARC_COMM_ID_BYTES 128
+int sparc_comm_unique_id(uint8_t *id_out);
+int sparc_comm_init(void *ctx, int32_t nranks, int32_t rank, const uint8_t *id, void **comm_out);
+int sparc_comm_destroy(void *comm);
+int sparc_gather_stats(void *ctx, void *comm, const int32_t *d_stats, int32_t *d_out);
 
 #ifdef __cplusplus
 }

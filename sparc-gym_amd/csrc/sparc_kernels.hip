@@ -10,6 +10,8 @@
 //   k_rules    rule audit of the current state                      (_validate_rules, 941-950)
 // No MFMA: this is integer / bitboard work, bound by latency and HBM.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <dlfcn.h>
 
 #include <algorithm>
 #include <cstdlib>
@@ -1013,6 +1015,7 @@ struct Ctx {
     int W = 1;
     bool loaded = false, has_state = false;
     uint32_t num_puzzles = 0, num_nodes = 0;
+    std::vector<uint32_t> h_info;      // host copy of the loaded table's info rows [P][4]
     // device buffers
     uint64_t *vis = nullptr, *dirs = nullptr;
     uint32_t *pos = nullptr, *aux = nullptr, *step = nullptr, *pid = nullptr;
@@ -1458,7 +1461,9 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
             }
             g.B = ((xmax + 2u) * g.P2 + 31u) / 32u + 1u;
             g.BS = (g.B + 3u) & ~3u;
-            g.M = c->cfg.traceback ? ((pts - 1u + 15u) & ~15u) : 0u;
+            // the move wave writes slot len - 1 on every step, moved or not, and len reaches pts
+            // on a path through every point: pts slots, not pts - 1
+            g.M = c->cfg.traceback ? ((pts + 15u) & ~15u) : 0u;
             g.nbr_pos = (2u * g.P2) | ((g.P2 - 1u) << 8) | (0u << 16) | ((g.P2 + 1u) << 24);
             g.off_board = (uint32_t)kW_Board;
             g.off_stack = g.off_board + g.BS * 256u;
@@ -1491,6 +1496,7 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
     }
     c->num_puzzles = (uint32_t)t->num_puzzles;
     c->num_nodes = (uint32_t)t->num_nodes;
+    c->h_info.assign(t->info, t->info + 4 * P);
     c->loaded = true;
     c->rules = false;       // the rule table indexes the old puzzles
     c->has_state = false;   // old state may point at puzzles that no longer exist
@@ -1956,6 +1962,41 @@ int sparc_set_visited_host(void* ctx, const uint64_t* visited) {
     int rc = check_ctx(c, true);
     if (rc) return rc;
     if (!visited) return fail(c, SPARC_E_INVALID, "null visited");
+    // every env's board must hold its start point (visited[start] = 1 at every load,
+    // SPaRC_Gym.py:185; no pop can clear it) and nothing outside its puzzle's lattice
+    const size_t n = c->n;
+    std::vector<uint32_t> pid(n);
+    HIPCHK(c, hipMemcpyAsync(pid.data(), c->pid, 4 * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const uint32_t pitch = (uint32_t)c->cfg.pitch;
+    const size_t W = (size_t)c->W;
+    std::vector<uint64_t> lat(c->num_puzzles * W, 0ull);   // each puzzle's lattice points
+    for (size_t q = 0; q < c->num_puzzles; ++q) {
+        const uint32_t w0 = c->h_info[4 * q], X = w0 & 0xFFu, Y = (w0 >> 8) & 0xFFu;
+        for (uint32_t x = 0; x < X; ++x)
+            for (uint32_t y = 0; y < Y; ++y) {
+                const uint32_t b = x * pitch + y;
+                lat[q * W + (b >> 6)] |= 1ull << (b & 63u);
+            }
+    }
+    for (size_t i = 0; i < n; ++i) {
+        const uint32_t q = pid[i];
+        if (q >= c->num_puzzles) return fail(c, SPARC_E_STATE, "env puzzle index out of range");
+        const uint32_t w0 = c->h_info[4 * (size_t)q];
+        const uint32_t X = w0 & 0xFFu, Y = (w0 >> 8) & 0xFFu, sb = ((w0 >> 16) & 0xFFu) * pitch + (w0 >> 24);
+        for (size_t k = 0; k < W; ++k) {
+            const uint64_t v = visited[k * n + i];
+            char m[128];
+            if (v & ~lat[q * W + k]) {
+                snprintf(m, sizeof m, "env %zu: visited bits outside its puzzle's %ux%u lattice", i, X, Y);
+                return fail(c, SPARC_E_INVALID, m);
+            }
+            if ((sb >> 6) == k && !((v >> (sb & 63u)) & 1ull)) {
+                snprintf(m, sizeof m, "env %zu: the start point is not set in visited", i);
+                return fail(c, SPARC_E_INVALID, m);
+            }
+        }
+    }
     HIPCHK(c, hipMemcpyAsync(c->vis, visited, sizeof(uint64_t) * c->W * c->n, hipMemcpyHostToDevice, c->stream));
     return sparc_sync(c);
 }
@@ -1989,6 +2030,117 @@ int sparc_copy_state_device(void* ctx, int32_t which, void* d_out) {
     const size_t n = c->n;
     const size_t bytes = which == 0 ? 8 * n * c->W : which == 5 ? 16 * n * c->W : 4 * n;
     HIPCHK(c, hipMemcpyAsync(d_out, src, bytes, hipMemcpyDeviceToDevice, c->stream));
+    return SPARC_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------------
+// End-of-batch collective over RCCL (xGMI between the GPUs of a node): one communicator per
+// process / GPU, one ncclAllGather of the per-env stats per rollout batch on the context's
+// stream (SURVEY §8b sparc_rccl_gather; the reference is single-process, llm_host.py:257-264).
+// librccl is opened on first use, so the library loads (and the step path runs) without it.
+namespace {
+struct Rccl {
+    bool tried = false, ok = false;
+    std::string why;
+    ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    const char* (*error_string)(ncclResult_t) = nullptr;
+};
+
+Rccl& rccl() {
+    static Rccl r;
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lock(mu);
+    if (r.tried) return r;
+    r.tried = true;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) {
+        const char* e = dlerror();
+        r.why = std::string("cannot open librccl: ") + (e ? e : "?");
+        return r;
+    }
+    r.get_unique_id = reinterpret_cast<decltype(r.get_unique_id)>(dlsym(h, "ncclGetUniqueId"));
+    r.comm_init_rank = reinterpret_cast<decltype(r.comm_init_rank)>(dlsym(h, "ncclCommInitRank"));
+    r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+    r.all_gather = reinterpret_cast<decltype(r.all_gather)>(dlsym(h, "ncclAllGather"));
+    r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(h, "ncclGetErrorString"));
+    r.ok = r.get_unique_id && r.comm_init_rank && r.comm_destroy && r.all_gather && r.error_string;
+    if (!r.ok) r.why = "librccl lacks an entry point (ncclGetUniqueId / CommInitRank / CommDestroy / AllGather)";
+    return r;
+}
+
+struct Comm {
+    ncclComm_t nc = nullptr;
+    int nranks = 0, rank = 0, device = -1;
+};
+
+#define RCCLCHK(c, expr)                                                                         \
+    do {                                                                                         \
+        ncclResult_t _r = (expr);                                                                \
+        if (_r != ncclSuccess)                                                                   \
+            return fail((c), SPARC_E_COMM, std::string(#expr ": ") + rccl().error_string(_r)); \
+    } while (0)
+}  // namespace
+
+extern "C" {
+
+int sparc_comm_unique_id(uint8_t* id_out) {
+    if (!id_out) return fail(nullptr, SPARC_E_INVALID, "null id_out");
+    Rccl& r = rccl();
+    if (!r.ok) return fail(nullptr, SPARC_E_COMM, r.why);
+    ncclUniqueId id;
+    RCCLCHK(nullptr, r.get_unique_id(&id));
+    memcpy(id_out, id.internal, SPARC_COMM_ID_BYTES);
+    return SPARC_OK;
+}
+
+int sparc_comm_init(void* ctx, int32_t nranks, int32_t rank, const uint8_t* id, void** comm_out) {
+    DevGuard dg;
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c || !id || !comm_out) return fail(c, SPARC_E_INVALID, "null argument");
+    *comm_out = nullptr;
+    if (nranks < 1 || rank < 0 || rank >= nranks) return fail(c, SPARC_E_INVALID, "need 0 <= rank < nranks");
+    Rccl& r = rccl();
+    if (!r.ok) return fail(c, SPARC_E_COMM, r.why);
+    HIPCHK(c, hipSetDevice(c->device));
+    ncclUniqueId uid;
+    memcpy(uid.internal, id, SPARC_COMM_ID_BYTES);
+    Comm* m = new Comm();
+    m->nranks = nranks;
+    m->rank = rank;
+    m->device = c->device;
+    const ncclResult_t rc = r.comm_init_rank(&m->nc, nranks, uid, rank);
+    if (rc != ncclSuccess) {
+        delete m;
+        return fail(c, SPARC_E_COMM, std::string("ncclCommInitRank: ") + r.error_string(rc));
+    }
+    *comm_out = m;
+    return SPARC_OK;
+}
+
+int sparc_comm_destroy(void* comm) {
+    DevGuard dg;
+    Comm* m = static_cast<Comm*>(comm);
+    if (!m) return SPARC_OK;
+    if (m->device >= 0) (void)hipSetDevice(m->device);
+    if (m->nc) (void)rccl().comm_destroy(m->nc);
+    delete m;
+    return SPARC_OK;
+}
+
+int sparc_gather_stats(void* ctx, void* comm, const int32_t* d_stats, int32_t* d_out) {
+    DevGuard dg;
+    Ctx* c = static_cast<Ctx*>(ctx);
+    Comm* m = static_cast<Comm*>(comm);
+    if (!c || !m || !d_stats || !d_out) return fail(c, SPARC_E_INVALID, "null argument");
+    if (m->device != c->device) return fail(c, SPARC_E_INVALID, "communicator and context are on different GPUs");
+    HIPCHK(c, hipSetDevice(c->device));
+    RCCLCHK(c, rccl().all_gather(d_stats, d_out, (size_t)4 * c->n, ncclInt32, m->nc, c->stream));
     return SPARC_OK;
 }
 

@@ -32,7 +32,8 @@ struct SplitGeom {
     uint32_t P2;        // internal pitch (<= 16: the window's right neighbour is bit 2 * P2 <= 32)
     uint32_t B;         // board dwords per lane (board + one zero dword above the top row)
     uint32_t BS;        // B rounded up to 4: dwords per lane in LDS and per puzzle in the reset-board table
-    uint32_t M;         // move-stack bytes per lane (>= the longest path's moves, multiple of 16)
+    uint32_t M;         // move-stack bytes per lane (>= the lattice's point count, multiple of 16:
+                        // a step writes slot len - 1 even when it does not move, and len <= points)
     uint32_t nbr_pos;   // window bit of each direction's neighbour, one byte per direction
     uint32_t pair;      // LDS bytes per move / trie wave pair
     uint32_t off_board, off_stack;   // their offsets within a pair

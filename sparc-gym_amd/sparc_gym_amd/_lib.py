@@ -71,7 +71,12 @@ _SIGS = {
     "sparc_load_rules": ([c_void_p, ctypes.POINTER(SparcRulesTable)], c_int32),
     "sparc_rules_device": ([c_void_p, c_void_p, c_void_p, c_void_p], c_int32),
     "sparc_rules_host": ([c_void_p, c_void_p, c_void_p, c_void_p], c_int32),
+    "sparc_comm_unique_id": ([c_void_p], c_int32),
+    "sparc_comm_init": ([c_void_p, c_int32, c_int32, c_void_p, ctypes.POINTER(c_void_p)], c_int32),
+    "sparc_comm_destroy": ([c_void_p], c_int32),
+    "sparc_gather_stats": ([c_void_p, c_void_p, c_void_p, c_void_p], c_int32),
 }
+COMM_ID_BYTES = 128   # SPARC_COMM_ID_BYTES
 EXPORTS = tuple(_SIGS)
 
 _lib = None

@@ -39,8 +39,9 @@ def init_from_env(backend="nccl", device=None):
 
 def gather_stats(stats: torch.Tensor, group=None) -> torch.Tensor:
     """End-of-batch gather: [N, 4] int32 per rank -> [world * N, 4] on every rank, ordered by
-    global env id.  A single all_gather (one RCCL call per batch, never per step)."""
-    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+    global env id.  A single all_gather (one RCCL call per batch, never per step); it runs
+    whenever a process group exists, world size 1 included (a copy)."""
+    if not dist.is_initialized():
         return stats
     world = dist.get_world_size(group)
     src = stats.contiguous()
@@ -55,6 +56,19 @@ def summarize(gathered: torch.Tensor) -> dict:
     """Totals over every env of every rank."""
     t = gathered.to(torch.int64).sum(0).cpu().tolist()
     return {"reward_code_sum": t[0], "done": t[1], "solved": t[2], "autoresets": t[3]}
+
+
+def gather_values(values, device=None):
+    """Every rank's list of numbers (same length on every rank) -> [[rank 0's], [rank 1's], ...]
+    (float64; one small all_gather).  Without a process group: [values]."""
+    if not dist.is_initialized():
+        return [list(map(float, values))]
+    if dist.get_backend() != "nccl":
+        device = "cpu"
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
+    out = torch.empty((dist.get_world_size(), t.numel()), dtype=torch.float64, device=device)
+    dist.all_gather_into_tensor(out, t)
+    return out.cpu().tolist()
 
 
 def max_over_ranks(seconds: float, device=None) -> float:

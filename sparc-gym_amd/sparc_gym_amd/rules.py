@@ -29,15 +29,19 @@ def region_map_of(region_bits, x_size, y_size, pitch):
 
 def rule_status(puzzle, obs_array, path, agent, target, bits, region_map, fit, terminated=False,
                 truncated=False):
-    """The reference's rule_status dict (structure of SPaRC_Gym.py:896-950)."""
-    if int(bits) & RULE_SEARCH_EXHAUSTED:
-        # the kernel caps each exact-fit search (sparc_rules.hpp kFitCap); past it the poly/ylop
-        # answer is unknown, and a guessed dict would silently differ from the reference's
-        raise RuntimeError("rule audit: the poly/ylop exact-fit search of this state passed its node cap "
-                           "(SPARC_RULE_SEARCH_EXHAUSTED); poly_ylop_area cannot be reported")
+    """The reference's rule_status dict (structure of SPaRC_Gym.py:896-950).
+
+    The kernel caps each exact-fit search (sparc_rules.hpp kFitCap).  Past the cap the poly/ylop
+    answer is unknown: rather than guess (a dict that silently differs from the reference's) or
+    abort the caller's episode, `poly_ylop_area` and `all_rules_satisfied` then report
+    ``passed=None`` and the poly detail carries ``"search_exhausted": True``."""
+    exhausted = bool(int(bits) & RULE_SEARCH_EXHAUSTED)
     color = np.asarray(puzzle["color_array"])
     add = np.asarray(puzzle["additional_info"])
     passed = {n: bool((int(bits) >> k) & 1) for k, n in enumerate(RULE_NAMES)}
+    if exhausted:
+        passed["poly_ylop_area"] = None
+        passed["all_rules_satisfied"] = None if all(passed[n] for n in RULE_NAMES[:7]) else False
     nreg = int(region_map.max()) + 1 if region_map.size and region_map.max() >= 0 else 0
     # _collect_region_symbols (456-481): per region, layer -> coords and colour -> count
     symbols = [dict() for _ in range(nreg)]
@@ -132,7 +136,10 @@ def rule_status(puzzle, obs_array, path, agent, target, bits, region_map, fit, t
                     if t != req:
                         mism.append({"x": x, "y": y, "required": req, "touches": t})
         add_rule("triangles_edge_count", {"mismatches": mism})
-    add_rule("poly_ylop_area", _poly_detail(puzzle, obs_array, add, region_map, area, fit))
+    poly = _poly_detail(puzzle, obs_array, add, region_map, area, fit)
+    if exhausted:
+        poly["search_exhausted"] = True
+    add_rule("poly_ylop_area", poly)
     core = [k for k in res]
     add_rule("all_rules_satisfied", {"rules_checked": core})
     res["_terminated"] = {"passed": True, "detail": terminated}

@@ -52,6 +52,18 @@ def test_null_context_is_an_error_not_a_crash():
     assert lib.sparc_destroy(None) == 0
 
 
+def test_comm_entry_points_validate_arguments():
+    """The RCCL gather's argument checks run before any RCCL or HIP call."""
+    lib = _lib.load()
+    comm = ctypes.c_void_p()
+    uid = (ctypes.c_uint8 * _lib.COMM_ID_BYTES)()
+    assert lib.sparc_comm_unique_id(None) == -1
+    assert lib.sparc_comm_init(None, 1, 0, uid, ctypes.byref(comm)) == -1
+    assert comm.value is None
+    assert lib.sparc_gather_stats(None, None, None, None) == -1
+    assert lib.sparc_comm_destroy(None) == 0
+
+
 def test_missing_library_fails_loudly(tmp_path):
     with pytest.raises(ImportError):
         _lib._lib = None

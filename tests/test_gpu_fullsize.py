@@ -191,3 +191,73 @@ def test_c4c_262144_envs_split_kernel_sampled_oracle(on_gpu):
                   ("outcome", "outcome")):
         assert np.array_equal(s[k][idx], so[ko]), k
     assert np.array_equal(visited_planes(s["visited"][:, idx], table, 16, 16), so["visited"].astype(np.int32))
+
+
+def _sharded_oracle_rollouts(proc, pids, acts_list, tb, ms, shards=16):
+    """The C oracle over column shards in threads (ctypes releases the GIL in the call): for
+    each launch's actions [T, n] (numpy), (reward codes, flags) [T, n]; returns them, the
+    accumulated stats [n, 4] and the concatenated final state."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import OraclePool
+    n = len(pids)
+    bounds = np.linspace(0, n, shards + 1).astype(int)
+    opool = OraclePool(_oracle_pool(proc))
+    oracles = [COracle(opool, int(b - a), tb, ms, autoreset=1) for a, b in zip(bounds[:-1], bounds[1:])]
+    stats = [np.zeros((int(b - a), 4), np.int32) for a, b in zip(bounds[:-1], bounds[1:])]
+    for o, a in zip(oracles, bounds[:-1]):
+        o.reset(pids[a:a + o.n])
+    outs = []
+    with ThreadPoolExecutor(shards) as ex:
+        for acts in acts_list:
+            T = acts.shape[0]
+            futs = [ex.submit(o.rollout, T, np.ascontiguousarray(acts[:, a:a + o.n]), 0, 0, 0, st)
+                    for o, a, st in zip(oracles, bounds[:-1], stats)]
+            res = [f.result() for f in futs]
+            outs.append((np.concatenate([r[0] for r in res], 1), np.concatenate([r[1] for r in res], 1)))
+    states = [o.state() for o in oracles]
+    state = {k: np.concatenate([s[k] for s in states]) for k in states[0]}
+    return outs, np.concatenate(stats), state
+
+
+def test_c3_bench_kernel_exact_instantiation_full_size(on_gpu):
+    """The bench's headline workload exactly (bench.py defaults, config c3): the c3 pool (1,024
+    puzzles, seed 0, full property set), 65,536 envs, env i -> puzzle i * 2654435761 mod 1024,
+    traceback, max_steps 2,000, next-step autoreset, uint8 actions drawn with torch.randint into
+    HBM by the bench's generator seed, and THREE back-to-back 2,000-step launches through the
+    same C-ABI call the bench times (sparc_rollout_device -> k_rollout1s<TB=1, RAND=0, LDS=1>:
+    65,536 = 256 whole 256-env workgroups, T % 16 == 0, the 1,024 puzzle rows staged in LDS),
+    the state round-tripping through HBM between launches.  Every env's reward codes, flags,
+    stats and final state must equal the C oracle (SPaRC_Gym.py:1111-1238)."""
+    from sparc_gym_amd import SPaRCVecEnv
+    proc, table = _bench_pool(((3, 3),), True)
+    n, T, L = 65536, 2000, 3
+    pids = _bench_pids(n)
+    v = SPaRCVecEnv(n, processed=proc, table=table, traceback=True, max_steps=2000, autoreset="next_step",
+                    observation="compact")
+    v.reset(options={"puzzle_index": pids})
+    assert table.words == 1 and len(proc) == 1024
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234)                                   # bench.py rank 0
+    acts = torch.randint(0, 4, (L, T, n), dtype=torch.uint8, device=dev, generator=g)
+    rew = torch.empty((L, T, n), dtype=torch.int8, device=dev)
+    flg = torch.empty((L, T, n), dtype=torch.uint8, device=dev)
+    stats = torch.zeros((n, 4), dtype=torch.int32, device=dev)
+    v._stream()
+    for k in range(L):                                    # as bench.run(): raw C-ABI calls, back to back
+        v.core.rollout_device(T, acts[k].data_ptr(), rew[k].data_ptr(), flg[k].data_ptr(), stats.data_ptr())
+    torch.cuda.synchronize()
+    v.core.sync()
+    acts_np = acts.cpu().numpy()
+    outs, ost, so = _sharded_oracle_rollouts(proc, pids, list(acts_np), True, 2000)
+    r_np, f_np = rew.cpu().numpy(), flg.cpu().numpy()
+    for k in range(L):
+        assert np.array_equal(r_np[k], outs[k][0]), f"reward codes differ in launch {k}"
+        assert np.array_equal(f_np[k], outs[k][1]), f"flags differ in launch {k}"
+    assert np.array_equal(stats.cpu().numpy(), ost)
+    _state_equal(v.state(), so, table)
+    # the workload exercised what the bench measures: episodes end at the target and by
+    # truncation, autoresets follow, and some episodes are solved
+    f_all = f_np.reshape(-1, n)
+    assert ((f_all & 1) != 0).sum() > 0 and ((f_all & 2) != 0).sum() > 0 and ((f_all & 64) != 0).sum() > 0
+    assert int(ost[:, 2].sum()) > 0

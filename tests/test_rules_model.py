@@ -84,20 +84,27 @@ def test_rule_status_layout_matches_reference(pool):
         assert rules_ref.normalize(got) == s["rule_status"], (pool, e, t)
 
 
-def test_exhausted_search_refuses_rule_status():
-    """An env whose exact-fit search hit the kernel's node cap (SPARC_RULE_SEARCH_EXHAUSTED) gets
-    no rule_status dict: its poly/ylop answer is unknown, so the host raises instead of guessing."""
+def test_exhausted_search_reports_unknown_poly_answer():
+    """An env whose exact-fit search hit the kernel's node cap (SPARC_RULE_SEARCH_EXHAUSTED) gets a
+    rule_status whose poly/ylop answer is marked unknown (passed None, search_exhausted in the
+    detail) instead of a guess, and the call does not abort the caller's episode."""
     import numpy as np
-    import pytest
     from collections import OrderedDict
-    from sparc_gym_amd.rules import RULE_SEARCH_EXHAUSTED, region_map_of, rule_status
+    from sparc_gym_amd.rules import RULE_NAMES, RULE_SEARCH_EXHAUSTED, region_map_of, rule_status
     g = load("rules_7x7_tb1")
     proc = process_puzzles(g["records"])
     table = pack_table(proc)
     p = proc[0]
     obs = OrderedDict((k, v.copy()) for k, v in p["obs_array"].items())
     reg = np.full(64 * table.words, 255, np.uint8)
-    with pytest.raises(RuntimeError, match="node cap"):
-        rule_status(p, obs, [list(p["start_location"])], np.array(p["start_location"]),
-                    np.array(p["target_location"]), RULE_SEARCH_EXHAUSTED,
-                    region_map_of(reg, p["x_size"], p["y_size"], table.pitch), 0)
+    args = (p, obs, [list(p["start_location"])], np.array(p["start_location"]), np.array(p["target_location"]))
+    rmap = region_map_of(reg, p["x_size"], p["y_size"], table.pitch)
+    # every other core rule passing: all_rules_satisfied is unknown too
+    other = sum(1 << k for k in range(7))
+    rs = rule_status(*args, RULE_SEARCH_EXHAUSTED | other, rmap, 0)
+    assert rs["poly_ylop_area"]["passed"] is None and rs["poly_ylop_area"]["detail"]["search_exhausted"]
+    assert rs["all_rules_satisfied"]["passed"] is None
+    assert all(rs[n]["passed"] is True for n in RULE_NAMES[:7])
+    # a failing core rule decides all_rules_satisfied whatever the poly answer
+    rs = rule_status(*args, RULE_SEARCH_EXHAUSTED | (other & ~1), rmap, 0)
+    assert rs["all_rules_satisfied"]["passed"] is False and rs["poly_ylop_area"]["passed"] is None
