@@ -75,6 +75,8 @@ struct Params {
     uint64_t env_offset;
     int32_t* __restrict__ err;
     uint32_t nbr_pos;   // W = 1: window bit of each direction's neighbour, one byte per direction
+    uint32_t nbm;       // W = 1 split move wave: mask of the four neighbour bits of the window
+    uint32_t lmagic;    // W = 1 split move wave: legal-bit gather constant (sparc_move1.hpp)
 };
 
 // Static puzzle rows, from global memory or from an LDS copy (same layout).  info.w holds the
@@ -458,10 +460,6 @@ struct Env<1, TB, Stack> {
     // solutions, done, reset step
     uint32_t s_a = 0, s_fwd = 0, s_pop = 0, s_mv = 0, s_done = 0, s_rs = 0;
     uint4 rec;
-    // k_rollout1s move wave: the row word and reset board of the puzzle the next autoreset
-    // loads, and the index of the one after it, read at the previous reset (reset_next_m)
-    uint32_t rpid = 0, rrow = 0;
-    uint64_t rinit = 0;
 
     // all arms are computed unconditionally and merged with masks: a C++ ?: whose arms are
     // 64-bit shifts is otherwise lowered to exec-masked if/else blocks
@@ -552,31 +550,6 @@ struct Env<1, TB, Stack> {
         }
     }
 
-    // reset_next with the next puzzle's row word and board already in registers (k_rollout1s
-    // move wave): they were read at the previous reset (or at load), so a reset waits on no
-    // read (MI355X, c3: 0.466 -> 0.460 ms per 2,000-step launch); a resetting lane then reads
-    // the row of the puzzle after the new one, for its next reset.  Move rows (split kernel):
-    // {row1.x, reset board lo, hi, the index of the puzzle after it}.  The move wave does not
-    // track the puzzle index (the trie wave does, and hands it over at the end).
-    __device__ __forceinline__ void prefetch_reset_m(const uint4* mrow, uint32_t q) {
-        const uint4 m = mrow[q];
-        rrow = m.x;
-        rinit = ((uint64_t)m.z << 32) | m.y;
-        rpid = m.w;
-    }
-    __device__ __forceinline__ void reset_next_m(const Params& p, const uint4* mrow) {
-        if (pending & (uint32_t)(p.autoreset == 1)) {
-            e = rrow & 0xFFu;
-            tgt = (rrow >> 8) & 0xFFu;
-            pflags = rrow >> 16;
-            bk = 0x7FFFFFFDu + ((~pflags >> 2) & 1u);
-            fr = rinit;
-            len = 1;
-            step = -1;   // this step's increment brings it to 0
-            rs = 1;
-            prefetch_reset_m(mrow, rpid);
-        }
-    }
     __device__ __forceinline__ uint32_t phase_move(const Params& p, uint32_t a) {
         const uint32_t P = p.pitch;
         step = __builtin_elementwise_add_sat(step, 1);                              // 1132
@@ -646,86 +619,6 @@ struct Env<1, TB, Stack> {
         outcome = done ? ((match | (outcome == 1)) ? 1u : 2u) : 0u;
         solved = (uint32_t)(done & match);
         return done ? c_done : c_move;
-    }
-
-    // ---- k_rollout1s move wave: phase_move with the split kernel's conventions (the rest of
-    // the state as phase_move):
-    //   * actions arrive sanitised to 0..4 (the I/O wave maps every byte >= 4 to 4, which reads
-    //     legal bit 4 = 0: never legal);
-    //   * with traceback the move stack is addressed through sp = this lane's slot len-1 (an
-    //     LDS byte address stepping 64 per move), and the traceback bias is folded into it:
-    //     (sp + bks) >> 31 is the len >= 3 or (len == 2, open start) test of legal_mask, so
-    //     len is not kept in the loop (the caller derives it from sp before store);
-    //   * it returns the hand-over word (flag byte | (fwd - pop) << 16) directly.
-    uint32_t sp = 0, bks = 0;   // sp: 32-bit LDS address
-    typedef __attribute__((address_space(3))) uint8_t lds_u8;
-    __device__ __forceinline__ static lds_u8* lds_byte(uint32_t a) { return (lds_u8*)(uintptr_t)a; }
-    __device__ __forceinline__ static uint32_t lds_addr(const uint8_t* g) { return (uint32_t)(uintptr_t)(lds_u8*)g; }
-    __device__ __forceinline__ void sp_from_len(uint32_t col_addr) {
-        sp = col_addr + (len - 1u) * 64u;
-        bks = 0x80000000u - col_addr - 128u + 64u * ((~pflags >> 2) & 1u);
-    }
-    __device__ __forceinline__ uint32_t legal_mask_s(uint32_t P) {
-        w = (uint32_t)(fr >> (e & 63u));
-        const uint32_t ud = __builtin_amdgcn_ubfe(w, P - 2u, 4u);
-        uint32_t m = (ud & 10u) | (((w << 2) & 4u) | __builtin_amdgcn_ubfe(w, 2u * P, 1u));
-        if constexpr (TB) m |= ((sp + bks) >> 31) << rl;
-        return m;
-    }
-    __device__ __forceinline__ void reset_next_s(const Params& p, const uint4* mrow, uint32_t col_addr) {
-        if (pending & (uint32_t)(p.autoreset == 1)) {
-            e = rrow & 0xFFu;
-            tgt = (rrow >> 8) & 0xFFu;
-            pflags = rrow >> 16;
-            fr = rinit;
-            sp = col_addr;                         // len = 1
-            len = 1;
-            bks = 0x80000000u - col_addr - 128u + 64u * ((~pflags >> 2) & 1u);
-            step = -1;   // this step's increment brings it to 0
-            rs = 1;
-            prefetch_reset_m(mrow, rpid);
-        }
-    }
-    __device__ __forceinline__ uint32_t phase_move_s(const Params& p, uint32_t a) {
-        const uint32_t P = p.pitch;
-        step = __builtin_elementwise_add_sat(step, 1);                              // 1132
-        const bool trunc0 = step >= p.max_steps;                                    // 1134
-        const uint32_t moved = (legal >> a) & (rs ^ 1u) & 1u;                       // 1137
-        const uint32_t pos = __builtin_amdgcn_ubfe(p.nbr_pos, a << 3, 8u);
-        const uint32_t pop = TB ? moved & ~__builtin_amdgcn_ubfe(w, pos, 1u) : 0u;  // 1141-1166
-        const uint32_t fwd = moved ^ pop;                                            // 1167-1188
-        const int32_t d = (int32_t)pos - (int32_t)P;
-        // free board: a forward move takes the target (bit e + P + d), a pop frees the point
-        // it leaves (bit e + P)
-        // only tog & 63 is used, so fwd * d may be taken mod 2^24: one full-rate v_mad_u32_u24
-        // (written out: the compiler selects fwd * d, in any spelling, as the quarter-rate
-        // v_mul_lo_u32)
-        uint32_t tog;
-        asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(tog) : "v"(fwd), "v"(d), "v"(e + P));
-        fr ^= (uint64_t)moved << (tog & 63u);
-        const int32_t dl = (int32_t)fwd - (int32_t)pop;
-        if constexpr (TB) {
-            const uint32_t ar = a ^ 2u;
-            *lds_byte(sp) = (uint8_t)ar;             // slot len-1
-            rl = fwd ? ar : (pop ? pnr : rl);
-            sp = (uint32_t)((int32_t)sp + __mul24(dl, 64));
-        } else {
-            len += fwd;   // no pops without traceback
-        }
-        e = (uint32_t)((int32_t)e + __mul24((int32_t)moved, d));
-        legal = legal_mask_s(P);
-        const uint32_t live = rs ^ 1u;
-        const bool at_tgt = e == tgt;                                                // 1192
-        const uint32_t term = at_tgt ? live : 0u;
-        const uint32_t done = (trunc0 | (legal == 0) | at_tgt) ? live : 0u;        // 1195-1199
-        pending = done;
-        // the move before the last (slot len-3 after the step; a harmless read of the slots
-        // below the stack when len < 3, where the traceback rule is off)
-        if constexpr (TB) pnr = *lds_byte(sp - 128u);
-        // flag bits: term | trunc << 1 = 2 * done - term (trunc = done and not term)
-        const uint32_t hw = (uint32_t)(dl << 16) | (rs << 6) | (legal << 2) | (2u * done - term);
-        rs = 0;
-        return hw;
     }
 
     // one whole step (k_step, and the generic-width interface)

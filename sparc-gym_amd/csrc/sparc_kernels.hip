@@ -25,6 +25,7 @@
 #include "sparc_env.hpp"
 #include "sparc_trie.hpp"
 #include "sparc_movew.hpp"
+#include "sparc_move1.hpp"
 #include "sparc_rules.hpp"
 #include "sparc_gym_amd.h"
 
@@ -614,22 +615,24 @@ __global__ void __launch_bounds__(kBlock1) k_rollout1(Params p, int32_t T, const
 //
 // A lone wave issues one instruction every ~5 cycles while its SIMD can take one every ~2.5
 // from two waves, and at 65,536 envs there is exactly one 64-env wave per SIMD.  So the step is
-// cut where its data flow is one-way: a MOVE wave runs the autoreset, legality, move, path and
-// flags (reset_next + phase_move) and hands each env-step over to a TRIE wave as one 32-bit LDS
-// word (hand_word32, sparc_trie.hpp); the trie wave (TrieLane) runs the solution-trie walk, the
-// record gathers, the reward code and the episode counters one 16-step tile behind.  Nothing
-// flows back: the reward code never feeds the move.  I/O waves stream action tiles in and
-// reward / flag tiles out.  Per workgroup 256 envs = 4 move waves (0-3) + 4 trie waves (4-7, on
+// cut where its data flow is one-way: a MOVE wave (MoveLane1, sparc_move1.hpp) runs the
+// autoreset, legality, move, path and flags and hands each env-step over to a TRIE wave as one
+// 32-bit LDS word; the trie wave (TrieLane::step1) runs the solution-trie walk, the record
+// gathers, the reward code and the episode counters one 16-step tile behind.  Nothing flows
+// back: the reward code never feeds the move.  I/O waves stream action tiles in (the actions
+// for the trie wave, each action's target window position for the move wave) and reward / flag
+// tiles out (the flag byte is byte 2 of the hand-over word).  Per workgroup 256 envs = 4 move waves (0-3) + 4 trie waves (4-7, on
 // the same SIMDs as the move waves of their envs) + 4 I/O waves (8-11, one per SIMD); one
 // barrier per tile:
 //   interval k (between barriers B_k and B_k+1): move waves step tile k; trie waves finish
 //   tile k-1; the I/O waves load the actions of tile k+1 and store the outputs of tile k-2.
-// Only full workgroups, T % 16 == 0 and 16-B aligned I/O; the host runs any tail through
-// k_rollout1.  The state after the launch is the same SoA record (the trie wave hands its
+// Only full workgroups, T % 16 == 0, 16-B aligned I/O and pitches 3..9 (split1_pitch_ok); the
+// host runs any tail (and other pools) through k_rollout1.  The state after the launch is the same SoA record (the trie wave hands its
 // final trie state and counters to the move wave through LDS before the store).
 constexpr int kBlock1s = 768;
-constexpr size_t kS_Act = 0;                          // actions [3 tiles][16][64]
-constexpr size_t kS_Rew = kS_Act + 3 * kTile * 64;    // reward ring [64 steps][64]
+constexpr size_t kS_Act = 0;                          // actions [3 tiles][16][64] (trie wave)
+constexpr size_t kS_Pos = kS_Act + 3 * kTile * 64;    // target window positions [3 tiles][16][64] (move wave)
+constexpr size_t kS_Rew = kS_Pos + 3 * kTile * 64;    // reward ring [64 steps][64]
 constexpr size_t kS_FH = kS_Rew + kRing * 64;         // hand-over ring [64 steps][64] u32
 constexpr size_t kS_Stk = kS_FH + 4 * kRing * 64;     // move stack [64 moves][64]
 constexpr size_t kS_Pair = kS_Stk + 64 * 64;          // per move / trie wave pair
@@ -647,10 +650,10 @@ __device__ __forceinline__ uint32_t clamp_actions4(uint32_t x) {
     return (x & ~bm) | (bm & 0x04040404u);
 }
 
-// the flag bytes (byte 0) of four hand-over words
+// the flag bytes (byte 2, sparc_move1.hpp) of four hand-over words
 __device__ __forceinline__ uint32_t flag_bytes4(const u32x4 w) {
-    const uint32_t lo = __builtin_amdgcn_perm(w.y, w.x, 0x0C0C0400u);
-    const uint32_t hi = __builtin_amdgcn_perm(w.w, w.z, 0x0C0C0400u);
+    const uint32_t lo = __builtin_amdgcn_perm(w.y, w.x, 0x0C0C0602u);
+    const uint32_t hi = __builtin_amdgcn_perm(w.w, w.z, 0x0C0C0602u);
     return lo | (hi << 16);
 }
 
@@ -685,6 +688,7 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         // issue load sat on one SIMD (MI355X, c3: 0.468 -> 0.466 ms per launch with four)
         const uint32_t io = wv - 8u;
         const uint32_t r = lane >> 2, c = (lane & 3u) * 16u;
+        const uint32_t pppp = p.pitch * 0x01010101u;
         auto load_tile = [&](int32_t k) {                        // actions of tile k -> buffer k % 3
             if constexpr (!RAND) {
                 u32x4 v = nt_load16(act + (size_t)(k * kTile + r) * n + wg_base + io * 64 + c);
@@ -692,7 +696,16 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
                 v.y = clamp_actions4(v.y);
                 v.z = clamp_actions4(v.z);
                 v.w = clamp_actions4(v.w);
-                *reinterpret_cast<u32x4*>(smem + io * kS_Pair + kS_Act + (k % 3) * (kTile * 64) + r * 64 + c) = v;
+                const size_t o = io * kS_Pair + (k % 3) * (kTile * 64) + r * 64 + c;
+                *reinterpret_cast<u32x4*>(smem + kS_Act + o) = v;
+                // the move wave's input: each action's target window position (byte a of
+                // nbr_pos; P, the agent's own never-free bit, for the illegal action 4)
+                u32x4 q;
+                q.x = __builtin_amdgcn_perm(pppp, p.nbr_pos, v.x);
+                q.y = __builtin_amdgcn_perm(pppp, p.nbr_pos, v.y);
+                q.z = __builtin_amdgcn_perm(pppp, p.nbr_pos, v.z);
+                q.w = __builtin_amdgcn_perm(pppp, p.nbr_pos, v.w);
+                *reinterpret_cast<u32x4*>(smem + kS_Pos + o) = q;
             }
         };
         auto store_tile = [&](int32_t k) {                       // whole 128-B lines, as k_rollout1
@@ -730,37 +743,39 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
     uint8_t* pb = smem + pr * kS_Pair;
     uint4* fin = reinterpret_cast<uint4*>(smem + kS_Fin) + 2u * (pr * 64u + lane);
     if (wv < 4) {                                                // ---- move waves
-        const PuzzleSrc<1> src{p.tab.info, p.tab.root, p.tab.open, p.tab.init, p.tab.row1};
-        Env<1, TB, typename std::conditional<TB, LdsStack<64>, RegStack>::type> e;
-        if constexpr (TB) e.stk.col = pb + kS_Stk + lane;
-        e.load(p, src, i);
-        e.prefetch_reset_m(mrow, e.pid + 1 == NP ? 0u : e.pid + 1);
-        const uint32_t pend0 = e.pending;
+        MoveLane1<TB> m;
+        uint8_t* col = pb + kS_Stk + lane;
+        const uint32_t col_addr = MoveLane1<TB>::lds_addr(col);
+        m.load(p, i, col, col_addr);
+        const uint32_t pid0 = p.st.pid[i];
+        m.prefetch_reset(mrow, pid0 + 1 == NP ? 0u : pid0 + 1);
+        const uint32_t pend0 = m.pending ? 1u : 0u;
         const uint64_t gid = p.env_offset + i;
         uint32_t* th = reinterpret_cast<uint32_t*>(pb + kS_FH) + lane;
-        const uint32_t col_addr = e.lds_addr(pb + kS_Stk + lane);
-        e.sp_from_len(col_addr);
         __syncthreads();                                         // B_0
         for (int32_t k = 0; k < K; ++k) {
-            // tile k's actions (buffer k % 3; the trie wave reads them one tile later)
+            // tile k's target positions (buffer k % 3; the trie wave reads the actions one tile
+            // later)
+            const uint8_t* tp = pb + kS_Pos + (k % 3) * (kTile * 64) + lane;
             uint8_t* ta = pb + kS_Act + (k % 3) * (kTile * 64) + lane;
 #pragma unroll 1
             for (int g = 0; g < kTile; g += 4) {
-                uint32_t av[4];
+                uint32_t pv[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     if constexpr (RAND) {
-                        av[j] = uint_rand_action(seed, gid, t0 + (uint64_t)(k * kTile + g + j));
-                        ta[(g + j) * 64] = (uint8_t)av[j];
+                        const uint32_t a = uint_rand_action(seed, gid, t0 + (uint64_t)(k * kTile + g + j));
+                        ta[(g + j) * 64] = (uint8_t)a;
+                        pv[j] = __builtin_amdgcn_ubfe(p.nbr_pos, a << 3, 8u);
                     } else {
-                        av[j] = ta[(g + j) * 64];
+                        pv[j] = tp[(g + j) * 64];
                     }
                 }
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const uint32_t row = (uint32_t)(k * kTile + g + j) & (kRing - 1);
-                    e.reset_next_s(p, mrow, col_addr);
-                    th[row * 64] = e.phase_move_s(p, av[j]);
+                    m.reset_next(p, mrow, col_addr);
+                    th[row * 64] = m.step_pos(p, pv[j]);
                 }
             }
             __syncthreads();                                     // B_{k+1}
@@ -769,15 +784,11 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         __syncthreads();                                         // B_{K+2}: the trie state is in fin
         const uint4 fs = fin[0];
         const uint4 fc = fin[1];
-        e.nn = fs.x & 0xFFFFu;
-        e.off = fs.x >> 16;
-        e.outcome = e.pending ? (fs.y == 0u ? 1u : 2u) : 0u;   // outcome_reward after the last step
-        e.pid = fc.y;
-        if constexpr (TB) e.len = (e.sp - col_addr) / 64u + 1u;
-        e.store(p, src, i);
+        const uint32_t pend = m.pending ? 1u : 0u;
+        m.store(p, i, col, col_addr, fs.x, pend ? (fs.y == 0u ? 1u : 2u) : 0u, fc.y);
         if (stats) {
             // autoresets: one per done step before the last, plus one for a done step carried in
-            const uint32_t resets = p.autoreset == 1 ? pend0 + fc.x - e.pending : 0u;
+            const uint32_t resets = p.autoreset == 1 ? pend0 + fc.x - pend : 0u;
             int4 st = stats[i];
             st.x += (int)fs.z;
             st.y += (int)fc.x;
@@ -809,7 +820,7 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
                     av[j] = ta[(g + j) * 64];
                 }
 #pragma unroll
-                for (int j = 0; j < 4; ++j) tr[(row0 + j) * 64] = (uint8_t)tl.step(hb[j], av[j], trow, p.tab.trie8, NP);
+                for (int j = 0; j < 4; ++j) tr[(row0 + j) * 64] = (uint8_t)tl.step1(hb[j], av[j], trow, p.tab.trie8, NP);
             }
             __syncthreads();                                     // B_{k+1}
         }
@@ -1105,6 +1116,10 @@ Params make_params(const Ctx* c) {
     p.err = c->err;
     const uint32_t P = p.pitch;
     p.nbr_pos = (2u * P) | ((P - 1u) << 8) | (0u << 16) | ((P + 1u) << 24);
+    if (c->W == 1 && split1_pitch_ok(P)) {
+        p.nbm = window_nbm(P);
+        p.lmagic = legal_magic(P);
+    }
     return p;
 }
 
@@ -1595,7 +1610,7 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
         // the full tiles of full workgroups go through the split move / trie kernel (MI355X, c3
         // at 65,536 envs: 0.266 vs 0.312 ms per 1,000 steps); a tail of T % 16 steps or a batch
         // that is not a multiple of 256 envs goes through k_rollout1 below
-        if (tiled && c->n % 256 == 0 && T >= kTile && c->t_trie8) {
+        if (tiled && c->n % 256 == 0 && T >= kTile && c->t_trie8 && split1_pitch_ok((uint32_t)c->cfg.pitch)) {
             const int32_t T16 = T / kTile * kTile;
             const size_t sbytes = split_table_bytes(c->num_puzzles);
             const bool lds_s = kS_Base + sbytes <= budget;

@@ -1,0 +1,218 @@
+// sparc_move1.hpp — the move wave of the W = 1 split rollout (k_rollout1s), device code.
+//
+// The split kernel runs each env's step() (SPaRC_Gym.py:1111-1238) over two waves: this MOVE
+// wave (legality, move or traceback pop, path, terminated / truncated) and the trie wave
+// (TrieLane, sparc_trie.hpp: solution trie, reward).  A lone wave issues in order, so every
+// instruction of the move wave's step lies on its time line; this lane keeps only what the
+// step's dependency chain needs and pushes the rest to the I/O wave and the host:
+//
+//  * the I/O wave hands over, per env-step, the WINDOW POSITION of the action's target instead
+//    of the action: pos = bit of the target point in the window w = fr >> e (right 2P, up P-1,
+//    left 0, down P+1; Env<1> in sparc_env.hpp explains the padded board, one row up), and P
+//    for an illegal action (>= 4): bit P of the window is the agent's own point, never free,
+//    so an illegal action tests "not free" and moves nowhere (SPaRC_Gym.py:1137);
+//  * a forward move is legal iff bit pos of w is set; the traceback pop (1141-1166) iff pos is
+//    the window position of path[-2] (rp, kept in a register) and the traceback rule holds
+//    (bias: len >= 3, or len == 2 with an open start);
+//  * the stack holds the back positions (2P - pos of each move), so the pop needs no
+//    direction arithmetic;
+//  * the legal-action mask (1024-1051) is not built in action order: its window bits
+//    lw = (w & NBM) | bias << rp are multiplied by one constant (p.lmagic) that carries the
+//    four bits right / up / left / down to bits 18..21 without carries (every partial product
+//    lands on its own bit), so the flag byte (term | trunc << 1 | legal << 2 | reset << 6)
+//    is byte 2 of the hand-over word and the I/O wave stores it with one byte select;
+//  * lw == 0 is the empty legal set (truncation, 1195).
+//
+// Hand-over word (to the trie wave and the I/O wave):
+//   bits 16..23  the flag byte (bit 16 terminated, 17 truncated, 18..21 legal, 22 autoreset)
+//   bits 30..31  fwd - pop, two's complement (+1 forward, -1 pop, 0 no move)
+//   other bits   0
+// Valid for pitches 3..9 (host-checked): the constant needs 2P <= 18.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sparc_env.hpp"
+
+namespace sparc {
+
+constexpr uint32_t kHwTerm = 0x10000u, kHwTrunc = 0x20000u, kHwReset = 0x400000u, kHwLegal = 0x3C0000u;
+
+// the carry-free gather constant and the neighbour mask of the window for pitch P (host and
+// device): window bits {2P, P-1, 0, P+1} -> product bits 18, 19, 20, 21 (right, up, left, down)
+__host__ __device__ constexpr uint32_t legal_magic(uint32_t P) {
+    return (1u << (18u - 2u * P)) + (1u << (20u - P)) + (1u << 20u);
+}
+__host__ __device__ constexpr uint32_t window_nbm(uint32_t P) {
+    return 1u | (1u << (P - 1u)) | (1u << (P + 1u)) | (1u << (2u * P));
+}
+__host__ __device__ constexpr bool split1_pitch_ok(uint32_t P) { return P >= 3u && P <= 9u; }
+
+// direction <-> window position of its neighbour (only at launch start / end)
+__device__ __forceinline__ uint32_t dir_pos1(uint32_t d, uint32_t P) {
+    return d == 0u ? 2u * P : d == 1u ? P - 1u : d == 2u ? 0u : P + 1u;
+}
+__device__ __forceinline__ uint32_t pos_dir1(uint32_t pos, uint32_t P) {
+    return pos == 2u * P ? 0u : pos == P - 1u ? 1u : pos == 0u ? 2u : 3u;
+}
+
+template <bool TB>
+struct MoveLane1 {
+    uint64_t fr = 0;          // free board, one row up (bit e + P = point e)
+    uint32_t e = 0, w = 0;    // agent bit; window (fr >> e) between steps, 0 on a reset step
+    uint32_t tgt = 0, pflags = 0, pending = 0, len = 1;
+    int32_t step = 0;
+    uint32_t sp = 0, bks = 0, bias = 0;   // traceback: stack slot len-1 (LDS byte address), rule bias
+    uint32_t rp = 0, pnr = 0;             // traceback: back position of the last move / the one before
+    uint32_t lv = 0x30000u;               // flag-bit mask of the step: term | trunc, or kHwReset
+    uint32_t rpid = 0, rrow = 0;          // the next autoreset's row word and the puzzle after it
+    uint64_t rinit = 0;                   // ... and its free board
+
+    typedef __attribute__((address_space(3))) uint8_t lds_u8;
+    __device__ __forceinline__ static lds_u8* lds_byte(uint32_t a) { return (lds_u8*)(uintptr_t)a; }
+    __device__ __forceinline__ static uint32_t lds_addr(const uint8_t* g) { return (uint32_t)(uintptr_t)(lds_u8*)g; }
+
+    __device__ __forceinline__ void set_bks(uint32_t col_addr) {
+        // (sp + bks) >> 31 = len >= 3, or len == 2 and the start is open (pflags bit 2 clear)
+        bks = 0x80000000u - col_addr - 128u + 64u * ((~pflags >> 2) & 1u);
+    }
+    __device__ __forceinline__ void prefetch_reset(const uint4* mrow, uint32_t q) {
+        const uint4 m = mrow[q];
+        rrow = m.x;
+        rinit = ((uint64_t)m.z << 32) | m.y;
+        rpid = m.w;
+    }
+
+    // gymnasium next-step autoreset (reset(), SPaRC_Gym.py:1087): the next puzzle's row and
+    // board from registers (read at the previous reset); the step then moves nowhere (w = 0,
+    // bias = 0) and reports the reset flag instead of term / trunc (lv)
+    __device__ __forceinline__ void reset_next(const Params& p, const uint4* mrow, uint32_t col_addr) {
+        if ((pending != 0u) & (p.autoreset == 1)) {
+            e = rrow & 0xFFu;
+            tgt = (rrow >> 8) & 0xFFu;
+            pflags = rrow >> 16;
+            fr = rinit;
+            w = 0;
+            if constexpr (TB) {
+                sp = col_addr;   // len = 1
+                set_bks(col_addr);
+                bias = 0;
+            } else {
+                len = 1;
+            }
+            step = -1;   // this step's increment brings it to 0
+            lv = kHwReset;
+            prefetch_reset(mrow, rpid);
+        }
+    }
+
+    // one env-step's move part (1131-1199) from the target's window position; returns the
+    // hand-over word
+    __device__ __forceinline__ uint32_t step_pos(const Params& p, uint32_t pos) {
+        const uint32_t P = p.pitch;
+        step = __builtin_elementwise_add_sat(step, 1);                              // 1132
+        const bool trunc0 = step >= p.max_steps;                                    // 1134
+        const uint32_t fwd = __builtin_amdgcn_ubfe(w, pos, 1u);                     // 1137, 1167
+        uint32_t pop = 0;
+        if constexpr (TB) pop = pos == rp ? bias : 0u;                              // 1141-1166
+        const uint32_t moved = fwd | pop;
+        const int32_t d = (int32_t)pos - (int32_t)P;
+        // free board: a forward move takes the target (bit e + P + d), a pop frees the point it
+        // leaves (bit e + P); fwd * d as one full-rate v_mad_u32_u24 (only tog & 63 is used)
+        uint32_t tog;
+        asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(tog) : "v"(fwd), "v"(d), "v"(e + P));
+        fr ^= (uint64_t)moved << (tog & 63u);
+        const int32_t dl = (int32_t)fwd - (int32_t)pop;
+        if constexpr (TB) {
+            const uint32_t arp = 2u * P - pos;         // back position of this move
+            *lds_byte(sp) = (uint8_t)arp;              // slot len-1: the new top if fwd
+            rp = fwd ? arp : (pop ? pnr : rp);
+            sp += (uint32_t)dl << 6;
+            bias = (sp + bks) >> 31;
+        } else {
+            len += fwd;
+        }
+        e = (uint32_t)((int32_t)e + __mul24((int32_t)moved, d));
+        w = (uint32_t)(fr >> (e & 63u));
+        // legal window bits; traceback: path[-2] (window bit rp) is legal although visited
+        uint32_t lw = w & p.nbm;
+        if constexpr (TB) lw |= bias << rp;
+        const bool at_tgt = e == tgt;                                                // 1192
+        const bool done = trunc0 | (lw == 0u) | at_tgt;                             // 1195-1199
+        // term | trunc << 1 at bits 16-17 (trunc = done and not term), or the reset bit
+        const uint32_t fb = (((done ? kHwTrunc : 0u) - (at_tgt ? kHwTerm : 0u)) | kHwReset) & lv;
+        pending = fb & (kHwTerm | kHwTrunc);
+        // the move before the last (slot len-3 after the step), for the next pop
+        if constexpr (TB) pnr = *lds_byte(sp - 128u);
+        lv = kHwTerm | kHwTrunc;
+        // lw * lmagic < 2^48 and only bits 18-21 are kept: v_mul_u32_u24, written out (the
+        // compiler selects the quarter-rate v_mul_lo_u32 for __umul24 here)
+        uint32_t prod;
+        asm("v_mul_u32_u24 %0, %1, %2" : "=v"(prod) : "v"(lw), "s"(p.lmagic));
+        return (prod & kHwLegal) | fb | ((uint32_t)dl << 30);
+    }
+
+    // ---- SoA <-> registers / LDS stack (launch start and end; the Env<1> state format)
+    __device__ __forceinline__ void load(const Params& p, uint32_t i, uint8_t* col, uint32_t col_addr) {
+        const State& s = p.st;
+        const uint32_t P = p.pitch;
+        const uint64_t vis = s.vis[i];
+        const uint32_t ps = s.pos[i], ax = s.aux[i];
+        const uint32_t pid = s.pid[i];
+        e = (ps & 0xFFu) * P + ((ps >> 8) & 0xFFu);
+        len = (ps >> 16) & 0xFFu;
+        pending = (ax >> 18) & 1u;
+        step = (int32_t)s.step[i];
+        const uint4 r = p.tab.row1[pid];
+        tgt = (r.x >> 8) & 0xFFu;
+        pflags = r.x >> 16;
+        fr = (p.tab.open[pid] & ~vis) << P;
+        w = (uint32_t)(fr >> (e & 63u));
+        lv = kHwTerm | kHwTrunc;
+        if constexpr (TB) {
+            const uint32_t moves = len >= 1 ? len - 1 : 0u;
+            const uint64_t lo = s.dirs[i], hi = s.dirs[(size_t)p.n + i];
+            for (uint32_t k = 0; k < moves; ++k) {
+                const uint32_t a = (uint32_t)(((k < 32 ? lo : hi) >> ((k & 31u) * 2u)) & 3u);
+                col[k * 64u] = (uint8_t)dir_pos1(a ^ 2u, P);
+            }
+            sp = col_addr + (len - 1u) * 64u;
+            set_bks(col_addr);
+            bias = (sp + bks) >> 31;
+            rp = len >= 2 ? col[(len - 2u) * 64u] : 0u;
+            pnr = *lds_byte(sp - 128u);
+        }
+    }
+
+    // S, outcome, pid: the trie wave's final trie state (off << 16 | packed node), outcome_reward
+    // and puzzle index
+    __device__ __forceinline__ void store(const Params& p, uint32_t i, const uint8_t* col, uint32_t col_addr,
+                                          uint32_t S, uint32_t outcome, uint32_t pid) {
+        const State& s = p.st;
+        const uint32_t P = p.pitch;
+        const uint64_t open = p.tab.open[pid];
+        const uint32_t sb = p.tab.row1[pid].x & 0xFFu;
+        // visited = in the puzzle and not free, plus the start (always on the path)
+        const uint64_t vis = ((~fr) >> P & open) | (1ull << sb);
+        s.vis[i] = vis;
+        if constexpr (TB) {
+            len = (sp - col_addr) / 64u + 1u;
+            uint64_t lo = 0, hi = 0;
+            for (uint32_t k = 0; k + 1 < len; ++k) {
+                const uint64_t v = (uint64_t)(pos_dir1(col[k * 64u], P) ^ 2u) << ((k & 31u) * 2u);
+                lo |= k < 32 ? v : 0ull;
+                hi |= k < 32 ? 0ull : v;
+            }
+            s.dirs[i] = lo;
+            s.dirs[(size_t)p.n + i] = hi;
+        }
+        const uint32_t x = e / P, y = e - x * P;
+        const uint32_t pend = pending ? 1u : 0u;
+        s.pos[i] = x | (y << 8) | (len << 16) | ((S >> 16) << 24);
+        s.aux[i] = (S & 0x7FFFu) | (outcome << 16) | (pend << 18) | (((S >> 15) & 1u) << 19);
+        s.step[i] = (uint32_t)step;
+        s.pid[i] = pid;
+    }
+};
+
+}  // namespace sparc

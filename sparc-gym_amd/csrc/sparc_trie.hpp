@@ -3,14 +3,12 @@
 // The solution-prefix test of step() (_is_on_solution_path, SPaRC_Gym.py:1244-1265, and the
 // np.array_equal test of 1206) walks a per-puzzle trie of the solution paths.  It needs from
 // the move wave only what the move did, so in the split kernels a TRIE wave runs it one tile
-// behind the move wave of the same 64 envs, from a 32-bit hand-over word per env-step and the
-// step's action (which the trie wave reads from the action tile itself):
-//
-//   bits  0-7   the flag byte   term | trunc << 1 | legal << 2 | autoreset << 6
-//   bits 16-31  fwd - pop       (+1 forward move, -1 traceback pop, 0 no move), 16-bit two's
-//                               complement (bit 16 = moved)
-//
-// so the move wave packs two fields (the flag byte it outputs anyway, and the move).
+// behind the move wave of the same 64 envs, from a hand-over word per env-step and the step's
+// action (which the trie wave reads from the action tile itself).  The word carries the flag
+// byte (term | trunc << 1 | legal << 2 | autoreset << 6) and fwd - pop (+1 forward move, -1
+// traceback pop, 0 no move); step() decodes the multi-word kernel's layout (widen_hand_word,
+// sparc_movew.hpp: flag byte at bits 0-7, fwd - pop at 16-31), step1() the W = 1 move wave's
+// (sparc_move1.hpp: flag byte at bits 16-23, fwd - pop at 30-31).
 //
 // Geometry-independent: the same lane serves the W = 1 and the multi-word kernels.
 //
@@ -74,11 +72,30 @@ struct TrieLane {
         nx = trow[npid];
     }
 
-    // one env-step from its hand-over word and action; returns the reward code (x100, 1201-1223)
+    // one env-step from its hand-over word (layout above) and action; returns the reward code
+    // (x100, 1201-1223)
     template <class Rows>
     __device__ __forceinline__ int step(const uint32_t hw, const uint32_t a, const Rows& trow,
                                         const uint2* __restrict__ trie8, uint32_t num_puzzles) {
-        if (hw & 0x40u) {   // autoreset step: the next puzzle's rows and its trie root
+        return step_core((hw & 0x40u) != 0u, hw & 0xFFFF0000u, hw >= 0x10000u, (hw & 3u) != 0u, a, trow, trie8,
+                         num_puzzles);
+    }
+    // the same from the W = 1 split move wave's word (sparc_move1.hpp): flag byte at bits 16-23,
+    // fwd - pop at bits 30-31 (sign-extended down to bits 16-31)
+    template <class Rows>
+    __device__ __forceinline__ int step1(const uint32_t hw, const uint32_t a, const Rows& trow,
+                                         const uint2* __restrict__ trie8, uint32_t num_puzzles) {
+        return step_core((hw & 0x400000u) != 0u, (uint32_t)((int32_t)hw >> 14) & 0xFFFF0000u, hw >= 0x40000000u,
+                         (hw & 0x30000u) != 0u, a, trow, trie8, num_puzzles);
+    }
+
+    // reset: an autoreset step; dd = (fwd - pop) << 16 (bit 16: moved); moved = dd != 0; done:
+    // terminated or truncated
+    template <class Rows>
+    __device__ __forceinline__ int step_core(const bool reset, const uint32_t dd, const bool moved, const bool done,
+                                             const uint32_t a, const Rows& trow, const uint2* __restrict__ trie8,
+                                             uint32_t num_puzzles) {
+        if (reset) {   // autoreset step: the next puzzle's rows and its trie root
             pid = npid;
             npid = next_pid(npid, num_puzzles);
             rx = nx.x;
@@ -97,7 +114,6 @@ struct TrieLane {
         // decides; off the trie (or without a child) the move counts the depth instead.
         const uint64_t xy = ((uint64_t)ry << 32) | rx;
         const uint32_t c = (uint32_t)(xy >> ((a << 4) & 0x30u));
-        const uint32_t dd = hw & 0xFFFF0000u;                  // (fwd - pop) << 16; bit 16: moved
         const uint32_t key = __builtin_amdgcn_ubfe(c, 0u, 16u) | (S & 0xFFFF0000u) | (~dd & 0x10000u);
         const bool take = key < 0xFFFFu;
         S = take ? key : S + dd;
@@ -114,8 +130,7 @@ struct TrieLane {
         // nor is done)
         const uint32_t x = S >> 15;                            // 0 on, 1 on a solution, >= 2 off
         const int cd = x == 1u ? 100 : Oneg;
-        const int cm = hw >= 0x10000u ? (x < 2u ? hs : hsn) : 0;
-        const bool done = (hw & 3u) != 0u;
+        const int cm = moved ? (x < 2u ? hs : hsn) : 0;
         const int code = done ? cd : cm;
         Oneg = done ? (cd < 0 ? cd : 0) : -100;
         acc_x += code;
@@ -124,10 +139,5 @@ struct TrieLane {
         return code;
     }
 };
-
-// the move wave's side of the hand-over word (see above)
-__device__ __forceinline__ uint32_t hand_word32(uint32_t fwd, uint32_t pop, uint32_t f) {
-    return ((fwd - pop) << 16) | f;
-}
 
 }  // namespace sparc

@@ -66,9 +66,9 @@ def gather_values(values, device=None):
     if dist.get_backend() != "nccl":
         device = "cpu"
     t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
-    out = torch.empty((dist.get_world_size(), t.numel()), dtype=torch.float64, device=device)
-    dist.all_gather_into_tensor(out, t)
-    return out.cpu().tolist()
+    out = torch.empty(dist.get_world_size() * t.numel(), dtype=torch.float64, device=device)
+    dist.all_gather_into_tensor(out, t)   # flat output: gloo takes no [world, n] shape
+    return out.view(dist.get_world_size(), t.numel()).cpu().tolist()
 
 
 def max_over_ranks(seconds: float, device=None) -> float:

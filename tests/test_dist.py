@@ -44,8 +44,9 @@ def _worker(rank, world, port, q):
     stats = torch.from_numpy(_run_shard(_pool(), offset, n))
     gathered = sdist.gather_stats(stats)
     t = sdist.max_over_ranks(0.1 * (r + 1))
+    vals = sdist.gather_values([r, 2.5 * r, 7])
     if r == 0:
-        q.put((gathered.numpy(), sdist.summarize(gathered), t))
+        q.put((gathered.numpy(), sdist.summarize(gathered), t, vals))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -63,7 +64,7 @@ def test_two_rank_gather_equals_single_process():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    gathered, summary, t = q.get(timeout=120)
+    gathered, summary, t, vals = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -71,6 +72,7 @@ def test_two_rank_gather_equals_single_process():
     assert np.array_equal(gathered, ref)
     assert summary["done"] == int(ref[:, 1].sum())
     assert t == pytest.approx(0.2)
+    assert vals == [[0.0, 0.0, 7.0], [1.0, 2.5, 7.0]]   # bench.py's per-rank records
 
 
 def test_shards_are_contiguous_and_disjoint():
