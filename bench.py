@@ -60,8 +60,12 @@ CONFIGS = {
     "c4c": (((2, 2), (3, 3), (4, 4), (5, 5)), True, True, False),
     # the other reading of "7x7": a 7x7 cell grid, i.e. a 15x15 lattice (SPaRC_Gym.py:243-248)
     "c3g7": (((7, 7),), True, True, False),
+    # c3 with the rule audit after every step, as the reference's full step() runs it
+    # (_validate_rules at SPaRC_Gym.py:1227 and 1011 -> info['rule_status'], 941-950)
+    "c3r": (((3, 3),), True, True, False),
 }
-DEFAULT_ENVS = {"c2": 4096, "c3": 65536, "c4": 262144, "c4c": 262144, "c3g7": 65536}
+RULE_CONFIGS = ("c3r",)
+DEFAULT_ENVS = {"c2": 4096, "c3": 65536, "c4": 262144, "c4c": 262144, "c3g7": 65536, "c3r": 65536}
 
 
 def parse():
@@ -90,6 +94,35 @@ def state_bytes_per_env(words, traceback):
     """HBM bytes one launch loads AND stores per env for its state (k_rollout / k_step):
     visited 8*words + dir stack 16*words (traceback) + pos/aux/step/pid 16."""
     return 8 * words + (16 * words if traceback else 0) + 16
+
+
+def cpu_baseline_rules(proc, tb, max_steps, seconds):
+    """The reference-speed full step() including its rule audit: oracle/cpu_ref.py's step core +
+    oracle/rules_ref.py's _validate_rules restatement once per step (the reference runs it twice,
+    SPaRC_Gym.py:1227 and 1011), pure Python, 1 thread, random actions, next-step reset."""
+    from oracle.cpu_ref import CpuRefEnv
+    from oracle import rules_ref
+    pool = [{"x_size": p["x_size"], "y_size": p["y_size"], "start": list(p["start_location"]),
+             "target": list(p["target_location"]), "solution_count": p["solution_count"],
+             "solution_paths": p["solution_paths"], "gaps": p["obs_array"]["gaps"]} for p in proc]
+    refp = [dict(p) for p in proc]
+    rng = np.random.default_rng(0)
+    q = 0
+    env = CpuRefEnv(pool[q], tb, max_steps)
+    k, t1 = 0, time.perf_counter()
+    while time.perf_counter() - t1 < seconds:
+        _, term, trunc = env.step(int(rng.integers(4)))
+        rules_ref.audit(refp[q], env.path, env.loc, term, trunc)
+        k += 1
+        if term or trunc:
+            q = (q + 1) % len(pool)
+            env.p = pool[q]
+            env.reset()
+    dt = time.perf_counter() - t1
+    return {"value": round(k / dt, 1), "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/cpu_ref.py step() + oracle/rules_ref.py rule audit once per step (pure Python, the "
+                      f"reference's algorithms), 1 env, {k} steps, random actions, {dt:.1f} s, 1 thread; CPU "
+                      f"{platform.processor() or platform.machine()}, os.cpu_count()={os.cpu_count()}"}
 
 
 def cpu_baseline(proc, tb, max_steps, seconds, obs_dims=None, config="c3"):
@@ -305,7 +338,8 @@ def main():
 
     K, W = max(1, args.steps), max(0, args.warmup)
     # env-steps per env in one bench step (one launch)
-    T = 1 if args.mode == "step" else (args.chunk if args.chunk > 0 else (50 if obs else 2000))
+    rules = args.config in RULE_CONFIGS
+    T = 1 if args.mode == "step" else (args.chunk if args.chunk > 0 else (50 if obs or rules else 2000))
     chunk = T
     # observation traces [T, N, x_dim, y_dim] int32 (visited, agent_location), reused by every
     # launch (a consumer reads them between launches)
@@ -322,6 +356,10 @@ def main():
     rew = torch.empty((RO, T, n), dtype=torch.int8, device=dev)
     flags = torch.empty((RO, T, n), dtype=torch.uint8, device=dev)
     stats = torch.zeros((n, 4), dtype=torch.int32, device=dev)
+    rbits = None
+    if rules:   # rule bits of every step [T, N] int16, as rollout(rules=True)
+        vec._load_rules()
+        rbits = torch.empty((RO, T, n), dtype=torch.int16, device=dev)
     stream = torch.cuda.current_stream(dev)
 
     vec._stream()                       # bind the context to this (torch's current) stream
@@ -340,6 +378,8 @@ def main():
                 core.step_device(ap, rp, fp)
             elif obs:
                 core.rollout_obs_device(T, ap, rp, fp, s_ptr, ovis.data_ptr(), oag.data_ptr(), X, Y)
+            elif rules:
+                core.rollout_rules_device(T, ap, rp, fp, s_ptr, rbits[k % RO].data_ptr())
             else:
                 core.rollout_device(T, ap, rp, fp, s_ptr)
             if ev:
@@ -378,11 +418,13 @@ def main():
     # launch the state (load + store) and, for rollouts, the stats record (load + store)
     sb = state_bytes_per_env(table.words, tb)
     per_env_launch = 2 * sb + (32 if args.mode == "rollout" else 0)
-    per_step = 3 + (2 * plane_bytes if obs and args.mode == "rollout" else 0)
+    per_step = 3 + (2 * plane_bytes if obs and args.mode == "rollout" else 0) + (2 if rules else 0)
     bytes_launch = n * (per_step * avg_T + per_env_launch)
     achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
     if args.mode != "rollout":
         kernel = "k_step"
+    elif rules:
+        kernel = "k_rollout"     # k_rollout<W, ..., RULES>: the audit after every step
     elif table.words == 1 and not obs:
         # batches of whole 256-env workgroups: the split move / trie kernel
         kernel = "k_rollout1s" if n % 256 == 0 and chunk >= 16 else "k_rollout1"
@@ -433,7 +475,9 @@ def main():
                                f"{'full property set' if full else 'base planes'}, traceback={tb}, "
                                f"max_steps={args.max_steps}, next-step autoreset, {args.puzzles} puzzles"
                                + (f", observation='new': visited + agent_location int32 planes "
-                                  f"[N, {X}, {Y}] written every step" if obs else ""),
+                                  f"[N, {X}, {Y}] written every step" if obs else "")
+                               + (", rule audit (info['rule_status'] bits, SPaRC_Gym.py:941-950) after "
+                                  "every step" if rules else ""),
                    "mode": args.mode, "envs_per_gpu": n, "env_steps_per_bench_step": T,
                    "env_steps_per_launch": T,
                    "parallelism": f"dp{world} (env shards, "
@@ -448,12 +492,17 @@ def main():
                      "algorithmic_bytes_per_launch": int(bytes_launch),
                      "bytes_model": f"per env-step {per_step} B (action, reward code, flags"
                                     f"{f', visited + agent_location planes 2 x {plane_bytes} B' if obs else ''}"
+                                    f"{', rule bits 2 B' if rules else ''}"
                                     f"); per env per launch "
                                     f"{per_env_launch} B (state {sb} B load+store"
                                     f"{', stats 16 B load+store' if args.mode == 'rollout' else ''})"},
         "episodes": summary,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and rules:
+        cb = cpu_baseline_rules(proc, tb, args.max_steps, args.cpu_seconds)
+        out["cpu_baseline"] = cb
+        out["gpu_vs_cpu"] = round(value / cb["value"], 1)
+    elif rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline(proc, tb, args.max_steps, args.cpu_seconds, (X, Y) if obs else None, args.config)
         out["cpu_baseline"] = cb
         out["gpu_vs_cpu"] = round(value / cb["value"], 1)

@@ -355,6 +355,8 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
                         ot.aout ? ot.aout + run : nullptr);
         }
     };
+    // exact-fit answers of this lane's recent regions (the path moves one point per step)
+    FitMemo<4> memo;
     auto audit_step = [&](int32_t t) {               // rule bits of the state after step t
         if constexpr (RULES) {
             uint64_t v[W];
@@ -364,7 +366,7 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
 #pragma unroll
             for (int k = 0; k < W; ++k) vb.w[k] = v[k];
             const uint32_t xy = e.agent_xy(p);
-            const RuleOut<W> ro = audit<W>(p, rtr.rt, vb, xy & 0xFFu, (xy >> 8) & 0xFFu, e.pid, nullptr);
+            const RuleOut<W> ro = audit<W>(p, rtr.rt, vb, xy & 0xFFu, (xy >> 8) & 0xFFu, e.pid, nullptr, &memo);
             rtr.bits[(size_t)t * n + i] = (uint16_t)ro.bits;
         }
     };

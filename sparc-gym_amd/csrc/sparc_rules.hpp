@@ -28,6 +28,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "sparc_env.hpp"
 
 namespace sparc {
@@ -146,20 +148,27 @@ __device__ __forceinline__ void fit_shape(const RulesTab& rt, uint32_t sh, uint3
         for (int ay = -mdy0; ay + mdy1 < (int)CY; ++ay) va |= 1ull << (ax * (int)CY + ay);
 }
 
+// the region's cells on the exact fit's cell grid (bit cx * CY + cy)
+template <int W>
+__device__ __forceinline__ uint64_t cell_mask(const FitIn& in, const BB<W>& Rc, uint32_t pitch) {
+    uint64_t rm = 0;
+    for (uint32_t cx = 0; cx < in.CX; ++cx)
+        for (uint32_t cy = 0; cy < in.CY; ++cy)
+            if (Rc.test((2 * cx + 1) * pitch + 2 * cy + 1)) rm |= 1ull << (cx * in.CY + cy);
+    return rm;
+}
+
 // _polyfit_region_exact with the area check passed (so net = area > 0 and the grid starts at
 // -1 on the region's cells), as a depth-first search over the same choices (existence only:
 // identical ylops take non-decreasing anchors, polys are tried by distinct shape).  Returns 1 (fits),
 // 0 (does not fit) or -1: the search passed kFitCap nodes without an answer (the env's audit
-// then reports SPARC_RULE_SEARCH_EXHAUSTED; the reference would keep searching)
+// then reports SPARC_RULE_SEARCH_EXHAUSTED; the reference would keep searching).  rm: the
+// region's cells (cell_mask).
 template <int W>
-__device__ __noinline__ int exact_fit(const FitIn& in, const BB<W>& Rc, uint32_t pitch) {
+__device__ __noinline__ int exact_fit(const FitIn& in, const BB<W>& Rc, uint64_t rm) {
     const RulesTab& rt = *in.rt;
     const uint32_t CX = in.CX, CY = in.CY;
     FitGrid g;
-    uint64_t rm = 0;
-    for (uint32_t cx = 0; cx < CX; ++cx)
-        for (uint32_t cy = 0; cy < CY; ++cy)
-            if (Rc.test((2 * cx + 1) * pitch + 2 * cy + 1)) rm |= 1ull << (cx * CY + cy);
 #pragma unroll
     for (int i = 0; i < kFitPlanes; ++i) g.p[i] = rm;    // -1 on the region
     uint32_t ysh[kFitYlops], dsh[kFitShapes];
@@ -244,6 +253,43 @@ __device__ __noinline__ int exact_fit(const FitIn& in, const BB<W>& Rc, uint32_t
     }
 }
 
+// Per-lane memo of exact-fit answers for the audit after every step of a rollout: the answer
+// depends only on the puzzle and the region's cells, and one step moves the path by one point,
+// so most regions (and their fit answers) carry over from the previous steps.  K entries of
+// (cell mask, answer) for one puzzle, replaced round robin; a miss runs the search.
+template <int K>
+struct FitMemo {
+    uint64_t key[K];
+    uint32_t res = 0, pid = ~0u, next = 0;
+    __device__ __forceinline__ FitMemo() {
+#pragma unroll
+        for (int k = 0; k < K; ++k) key[k] = 0;   // a region holds cells: its mask is never 0
+    }
+    // 1 / 0: the memoised answer, -1: not known
+    __device__ __forceinline__ int find(uint32_t q, uint64_t rm) const {
+        int r = -1;
+#pragma unroll
+        for (int k = 0; k < K; ++k) r = (q == pid && key[k] == rm) ? (int)((res >> k) & 1u) : r;
+        return r;
+    }
+    __device__ __forceinline__ void put(uint32_t q, uint64_t rm, int fits) {
+        if (q != pid) {
+            pid = q;
+#pragma unroll
+            for (int k = 0; k < K; ++k) key[k] = 0;
+            next = 0;
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const bool here = next == (uint32_t)k;
+            key[k] = here ? rm : key[k];
+            res = here ? ((res & ~(1u << k)) | ((uint32_t)fits << k)) : res;
+        }
+        next = next + 1 == (uint32_t)K ? 0u : next + 1;
+    }
+};
+struct NoMemo {};
+
 // ---------------------------------------------------------------- the audit
 template <int W>
 struct RuleOut {
@@ -252,9 +298,10 @@ struct RuleOut {
 };
 
 // vis: path points; x, y: agent; q: puzzle.  region_out (may be null): region id per bit.
-template <int W>
+// memo (FitMemo, or NoMemo): exact-fit answers carried between calls of one lane.
+template <int W, class Memo = NoMemo>
 __device__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const BB<W>& vis, uint32_t x, uint32_t y,
-                            uint32_t q, uint8_t* region_out) {
+                            uint32_t q, uint8_t* region_out, Memo* memo = nullptr) {
     // every plane of the puzzle in registers up front: one round of loads, none in the loops
     BB<W> pl[RP_COUNT];
     {
@@ -332,7 +379,14 @@ __device__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const BB<W>& vi
         if (has) {
             bool ok = Rc.popc() == pa - ya;
             if (ok) {
-                const int r = exact_fit<W>(fin, Rc, P);
+                const uint64_t rm = cell_mask<W>(fin, Rc, P);
+                int r = -1;
+                if constexpr (!std::is_same<Memo, NoMemo>::value) r = memo->find(q, rm);
+                if (r < 0) {
+                    r = exact_fit<W>(fin, Rc, rm);
+                    if constexpr (!std::is_same<Memo, NoMemo>::value)
+                        if (r >= 0) memo->put(q, rm, r);
+                }
                 exhausted |= r < 0;
                 ok = r > 0;
             }

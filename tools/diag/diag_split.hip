@@ -56,172 +56,45 @@ struct DiagTrieLane : TrieLane {
     }
 };
 
+
+// MoveLane1 with the autoreset variants: MV 0 the product's (divergent branch), 1 none (timing
+// only), 2 a wave-uniform branch around it (no exec save / restore when no lane resets), 3
+// branch-free selects with the next reset row read every step
+template <bool TB, int MV>
+struct DiagMoveLane1 : MoveLane1<TB> {
+    using B = MoveLane1<TB>;
+    __device__ __forceinline__ void reset_v(const Params& p, const uint4* mrow, uint32_t col_addr) {
+        if constexpr (MV == 0) {
+            B::reset_next(p, mrow, col_addr);
+        } else if constexpr (MV == 2) {
+            if (__builtin_amdgcn_ballot_w64((B::pending != 0u) & (p.autoreset == 1))) B::reset_next(p, mrow, col_addr);
+        } else if constexpr (MV == 3) {
+            const bool rs = (B::pending != 0u) & (p.autoreset == 1);
+            const uint4 nx = mrow[B::rpid];
+            B::e = rs ? (B::rrow & 0xFFu) : B::e;
+            B::tgt = rs ? ((B::rrow >> 8) & 0xFFu) : B::tgt;
+            B::pflags = rs ? (B::rrow >> 16) : B::pflags;
+            B::fr = rs ? B::rinit : B::fr;
+            B::w = rs ? 0u : B::w;
+            if constexpr (TB) {
+                B::sp = rs ? col_addr : B::sp;
+                B::bks = rs ? 0x80000000u - col_addr - 128u + 64u * ((~(B::rrow >> 16) >> 2) & 1u) : B::bks;
+                B::bias = rs ? 0u : B::bias;
+            } else {
+                B::len = rs ? 1u : B::len;
+            }
+            B::step = rs ? -1 : B::step;
+            B::lv = rs ? kHwReset : B::lv;
+            B::rrow = rs ? nx.x : B::rrow;
+            B::rinit = rs ? (((uint64_t)nx.z << 32) | nx.y) : B::rinit;
+            B::rpid = rs ? nx.w : B::rpid;
+        }
+    }
+};
+
 // per wave: [0] cycles working (barrier release -> next barrier arrival), [1] cycles waiting at
-// barriers, [2] cycles in the whole tile loop, [3] tiles
-template <bool TB, int G>
-__global__ void __launch_bounds__(kBlock1s) k_rollout1s_diag(Params p, int32_t T, const uint8_t* __restrict__ act,
-                                                             int8_t* __restrict__ rew, uint8_t* __restrict__ flg,
-                                                             int4* __restrict__ stats, uint64_t* __restrict__ times) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const uint32_t NP = p.tab.num_puzzles;
-    uint4* lm = reinterpret_cast<uint4*>(smem + kS_Base);
-    uint4* lt = lm + NP;
-    for (uint32_t k = threadIdx.x; k < NP; k += kBlock1s) {
-        lm[k] = p.tab.mrow[k];
-        lt[k] = p.tab.trow[k];
-    }
-    __syncthreads();
-    const uint4* mrow = lm;
-    const uint4* trow = lt;
-    const size_t n = p.n;
-    const uint32_t wg_base = blockIdx.x * 256u;
-    const int32_t K = T / kTile;
-    uint64_t t_work = 0, t_bar = 0, t_all = 0, tiles = 0;
-    uint64_t t0 = stamp();
-    const uint64_t start = t0;
-    auto bar = [&]() {          // one barrier, stamped
-        const uint64_t a = stamp();
-        t_work += a - t0;
-        __syncthreads();
-        t0 = stamp();
-        t_bar += t0 - a;
-        ++tiles;
-    };
-    auto flush = [&]() {
-        t_all = stamp() - start;
-        if (lane == 0) {
-            uint64_t* o = times + ((size_t)blockIdx.x * 12u + wv) * 4u;
-            o[0] = t_work;
-            o[1] = t_bar;
-            o[2] = t_all;
-            o[3] = tiles;
-        }
-    };
-    if (wv >= 8) {
-        const uint32_t io = wv - 8u;
-        const uint32_t r = lane >> 2, c = (lane & 3u) * 16u;
-        const uint32_t pppp = p.pitch * 0x01010101u;
-        auto load_tile = [&](int32_t k) {
-            u32x4 v = nt_load16(act + (size_t)(k * kTile + r) * n + wg_base + io * 64 + c);
-            v.x = clamp_actions4(v.x);
-            v.y = clamp_actions4(v.y);
-            v.z = clamp_actions4(v.z);
-            v.w = clamp_actions4(v.w);
-            const size_t o = io * kS_Pair + (k % 3) * (kTile * 64) + r * 64 + c;
-            *reinterpret_cast<u32x4*>(smem + kS_Act + o) = v;
-            u32x4 q;
-            q.x = __builtin_amdgcn_perm(pppp, p.nbr_pos, v.x);
-            q.y = __builtin_amdgcn_perm(pppp, p.nbr_pos, v.y);
-            q.z = __builtin_amdgcn_perm(pppp, p.nbr_pos, v.z);
-            q.w = __builtin_amdgcn_perm(pppp, p.nbr_pos, v.w);
-            *reinterpret_cast<u32x4*>(smem + kS_Pos + o) = q;
-        };
-        auto store_tile = [&](int32_t k) {
-            const uint32_t r8 = lane >> 3, c8 = (lane & 7u) * 16u;
-            const uint32_t h = io >> 1, q = io & 1u;
-            const uint32_t row = (uint32_t)((k * kTile) & (kRing - 1)) + h * 8 + r8;
-            const uint32_t w = 2 * q + (c8 >> 6);
-            const uint8_t* base = smem + w * kS_Pair + row * 64 + (c8 & 63u);
-            const size_t o = (size_t)(k * kTile + h * 8 + r8) * n + wg_base + q * 128 + c8;
-            nt_store16(reinterpret_cast<uint8_t*>(rew) + o, *reinterpret_cast<const u32x4*>(base + kS_Rew));
-            const u32x4* fh = reinterpret_cast<const u32x4*>(smem + w * kS_Pair + kS_FH + row * 256 + 4 * (c8 & 63u));
-            u32x4 v;
-            v.x = flag_bytes4(fh[0]);
-            v.y = flag_bytes4(fh[1]);
-            v.z = flag_bytes4(fh[2]);
-            v.w = flag_bytes4(fh[3]);
-            nt_store16(flg + o, v);
-        };
-        if (K > 0) load_tile(0);
-        bar();
-        for (int32_t k = 0; k <= K; ++k) {
-            if (k + 1 < K) load_tile(k + 1);
-            if (k >= 2) store_tile(k - 2);
-            bar();
-        }
-        if (K >= 1) store_tile(K - 1);
-        bar();
-        flush();
-        return;
-    }
-    const uint32_t pr = wv & 3u;
-    const uint32_t i = wg_base + pr * 64u + lane;
-    uint8_t* pb = smem + pr * kS_Pair;
-    uint4* fin = reinterpret_cast<uint4*>(smem + kS_Fin) + 2u * (pr * 64u + lane);
-    if (wv < 4) {
-        MoveLane1<TB> m;
-        uint8_t* col = pb + kS_Stk + lane;
-        const uint32_t col_addr = MoveLane1<TB>::lds_addr(col);
-        m.load(p, i, col, col_addr);
-        const uint32_t pid0 = p.st.pid[i];
-        m.prefetch_reset(mrow, pid0 + 1 == NP ? 0u : pid0 + 1);
-        const uint32_t pend0 = m.pending ? 1u : 0u;
-        uint32_t* th = reinterpret_cast<uint32_t*>(pb + kS_FH) + lane;
-        bar();
-        for (int32_t k = 0; k < K; ++k) {
-            const uint8_t* tp = pb + kS_Pos + (k % 3) * (kTile * 64) + lane;
-#pragma unroll 1
-            for (int g = 0; g < kTile; g += 4) {
-                uint32_t pv[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) pv[j] = tp[(g + j) * 64];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const uint32_t row = (uint32_t)(k * kTile + g + j) & (kRing - 1);
-                    m.reset_next(p, mrow, col_addr);
-                    th[row * 64] = m.step_pos(p, pv[j]);
-                }
-            }
-            bar();
-        }
-        bar();
-        bar();
-        const uint4 fs = fin[0];
-        const uint4 fc = fin[1];
-        const uint32_t pend = m.pending ? 1u : 0u;
-        m.store(p, i, col, col_addr, fs.x, pend ? (fs.y == 0u ? 1u : 2u) : 0u, fc.y);
-        if (stats) {
-            const uint32_t resets = p.autoreset == 1 ? pend0 + fc.x - pend : 0u;
-            int4 st = stats[i];
-            st.x += (int)fs.z;
-            st.y += (int)fc.x;
-            st.z += (int)fs.w;
-            st.w += (int)resets;
-            stats[i] = st;
-        }
-        flush();
-    } else {
-        __builtin_amdgcn_s_setprio(1);
-        DiagTrieLane<G> tl;
-        tl.lds_rows = lt;
-        tl.load(p.st.pos[i], p.st.aux[i], p.st.pid[i], trow, p.tab.trie8, NP);
-        const uint32_t* th = reinterpret_cast<const uint32_t*>(pb + kS_FH) + lane;
-        uint8_t* tr = pb + kS_Rew + lane;
-        bar();
-        bar();
-        for (int32_t k = 1; k <= K; ++k) {
-            const uint8_t* ta = pb + kS_Act + ((k - 1) % 3) * (kTile * 64) + lane;
-#pragma unroll 1
-            for (int g = 0; g < kTile; g += 4) {
-                const uint32_t row0 = (uint32_t)((k - 1) * kTile + g) & (kRing - 1);
-                uint32_t hb[4], av[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    hb[j] = th[(row0 + j) * 64];
-                    av[j] = ta[(g + j) * 64];
-                }
-#pragma unroll
-                for (int j = 0; j < 4; ++j) tr[(row0 + j) * 64] = (uint8_t)tl.step1d(hb[j], av[j], trow, p.tab.trie8, NP);
-            }
-            bar();
-        }
-        fin[0] = make_uint4(tl.S, (uint32_t)tl.Oneg, (uint32_t)tl.acc_x, tl.acc_z);
-        fin[1] = make_uint4(tl.acc_y, tl.pid, 0u, 0u);
-        bar();
-        flush();
-    }
-}
+// barriers, [2] cycles in the whole kernel after the prologue, [3] barriers
+#include "diag_kernel.inc"
 
 }  // namespace
 
@@ -233,24 +106,33 @@ extern "C" int sparc_diag_rollout1s(void* ctx, int32_t T, const uint8_t* d_act, 
     if (c->W != 1 || c->n % 256 || T % kTile || !d_act || !d_rew || !d_flags || !d_times)
         return fail(c, SPARC_E_INVALID, "diag: W = 1, whole workgroups, whole tiles, all buffers");
     const Params p = make_params(c);
+    if (!split1_pitch_ok(p.pitch)) return fail(c, SPARC_E_INVALID, "diag: pitch outside 3..9");
     const size_t shm = kS_Base + split_table_bytes(c->num_puzzles);
     if (shm > kMaxDynLds) return fail(c, SPARC_E_INVALID, "diag: table does not fit LDS");
     auto go = [&](auto kern) {
         rc = allow_big_lds(c, reinterpret_cast<const void*>(kern));
         if (rc) return;
-        kern<<<dim3(c->n / 256), kBlock1s, shm, c->stream>>>(p, T, d_act, d_rew, d_flags,
+        kern<<<dim3(c->n / 256), kBlock1s, shm, c->stream>>>(p, T, d_act, 0, 0, d_rew, d_flags,
                                                             reinterpret_cast<int4*>(d_stats), d_times);
     };
-    // variant: the trie wave's record gather, 0 = global (the product's), 1 = LDS, 2 = none
-    if (c->cfg.traceback) {
-        if (variant == 1) go(k_rollout1s_diag<true, 1>);
-        else if (variant == 2) go(k_rollout1s_diag<true, 2>);
-        else go(k_rollout1s_diag<true, 0>);
-    } else {
-        if (variant == 1) go(k_rollout1s_diag<false, 1>);
-        else if (variant == 2) go(k_rollout1s_diag<false, 2>);
-        else go(k_rollout1s_diag<false, 0>);
-    }
+    // variant % 10: the trie wave's record gather, 0 = global (the product's), 1 = LDS, 2 = none;
+    // variant / 10: the move wave's autoreset (DiagMoveLane1)
+    const int g = variant % 10, mv = variant / 10;
+    auto pick = [&](auto tb) {
+        constexpr bool TB = decltype(tb)::value;
+        auto pg = [&](auto mvc) {
+            constexpr int MV = decltype(mvc)::value;
+            if (g == 1) go(k_rollout1s_diag<TB, false, true, 1, MV>);
+            else if (g == 2) go(k_rollout1s_diag<TB, false, true, 2, MV>);
+            else go(k_rollout1s_diag<TB, false, true, 0, MV>);
+        };
+        if (mv == 1) pg(std::integral_constant<int, 1>{});
+        else if (mv == 2) pg(std::integral_constant<int, 2>{});
+        else if (mv == 3) pg(std::integral_constant<int, 3>{});
+        else pg(std::integral_constant<int, 0>{});
+    };
+    if (c->cfg.traceback) pick(std::true_type{});
+    else pick(std::false_type{});
     if (rc) return rc;
     return launch_check(c);
 }

@@ -18,7 +18,8 @@ import torch  # noqa: E402
 torch.cuda.init()
 from sparc_gym_amd import _lib  # noqa: E402
 
-lib = _lib.load(os.path.join(REPO, "tools", "diag", "libsparc_diag.so"))
+_name = sys.argv[sys.argv.index("--diag-lib") + 1] if "--diag-lib" in sys.argv else "libsparc_diag.so"
+lib = _lib.load(os.path.join(REPO, "tools", "diag", _name))
 lib.sparc_diag_rollout1s.argtypes = [ctypes.c_void_p, ctypes.c_int32] + [ctypes.c_void_p] * 5 + [ctypes.c_int32]
 lib.sparc_diag_rollout1s.restype = ctypes.c_int32
 
@@ -31,6 +32,7 @@ ap.add_argument("--config", default="c3")
 ap.add_argument("--envs", type=int, default=65536)
 ap.add_argument("--chunk", type=int, default=2000)
 ap.add_argument("--launches", type=int, default=4)
+ap.add_argument("--diag-lib", default="libsparc_diag.so")
 ap.add_argument("--variant", type=int, default=0, help="trie gather: 0 global (product), 1 LDS (fake records), 2 none")
 a = ap.parse_args()
 sizes, full, tb, obs = bench.CONFIGS[a.config]
