@@ -85,8 +85,13 @@ struct MoveLane1 {
 
     // gymnasium next-step autoreset (reset(), SPaRC_Gym.py:1087): the next puzzle's row and
     // board from registers (read at the previous reset); the step then moves nowhere (w = 0,
-    // bias = 0) and reports the reset flag instead of term / trunc (lv)
+    // bias = 0) and reports the reset flag instead of term / trunc (lv).  The row of the reset
+    // after it is read on every step, outside the branch: read inside, the branch waits for it
+    // (it lands in temporaries and is copied on), and about a fifth of all wave-steps take the
+    // branch (MI355X, per-role stamps of tools/diag_split.py: the move wave's step 421.8 ->
+    // 409.3 cycles at 65,536 envs)
     __device__ __forceinline__ void reset_next(const Params& p, const uint4* mrow, uint32_t col_addr) {
+        const uint4 nx = mrow[rpid];
         if ((pending != 0u) & (p.autoreset == 1)) {
             e = rrow & 0xFFu;
             tgt = (rrow >> 8) & 0xFFu;
@@ -102,7 +107,9 @@ struct MoveLane1 {
             }
             step = -1;   // this step's increment brings it to 0
             lv = kHwReset;
-            prefetch_reset(mrow, rpid);
+            rrow = nx.x;
+            rinit = ((uint64_t)nx.z << 32) | nx.y;
+            rpid = nx.w;
         }
     }
 

@@ -9,7 +9,8 @@ namespace {
 __device__ __forceinline__ uint64_t stamp() { return __builtin_amdgcn_s_memtime(); }
 
 // TrieLane with the record gather replaced (G = 1: from an LDS table, valid memory but fake
-// records; G = 2: no gather, the record stays): timing only, the outputs are wrong
+// records; G = 2: no gather, the record stays: timing only, the outputs are wrong; G = 3: the
+// current node's record reloaded every step, no exec-masked branch: correct)
 template <int G>
 struct DiagTrieLane : TrieLane {
     const uint4* lds_rows = nullptr;
@@ -43,6 +44,10 @@ struct DiagTrieLane : TrieLane {
                 rx = r.x;
                 ry = r.y;
             }
+        } else if constexpr (G == 3) {   // every step: the current node's record (unchanged unless taken)
+            const uint2 rec = trie8[base + (S & 0x7FFFu)];
+            rx = rec.x;
+            ry = rec.y;
         }
         const uint32_t x = S >> 15;
         const int cd = x == 1u ? 100 : Oneg;
@@ -68,6 +73,44 @@ struct DiagMoveLane1 : MoveLane1<TB> {
             B::reset_next(p, mrow, col_addr);
         } else if constexpr (MV == 2) {
             if (__builtin_amdgcn_ballot_w64((B::pending != 0u) & (p.autoreset == 1))) B::reset_next(p, mrow, col_addr);
+        } else if constexpr (MV == 4) {   // the branch without the next-row prefetch (timing only)
+            if ((B::pending != 0u) & (p.autoreset == 1)) {
+                B::e = B::rrow & 0xFFu;
+                B::tgt = (B::rrow >> 8) & 0xFFu;
+                B::pflags = B::rrow >> 16;
+                B::fr = B::rinit;
+                B::w = 0;
+                if constexpr (TB) {
+                    B::sp = col_addr;
+                    B::set_bks(col_addr);
+                    B::bias = 0;
+                } else {
+                    B::len = 1;
+                }
+                B::step = -1;
+                B::lv = kHwReset;
+            }
+        } else if constexpr (MV == 5) {   // the next-row prefetch every step, outside the branch
+            const uint4 nx = mrow[B::rpid];
+            if ((B::pending != 0u) & (p.autoreset == 1)) {
+                B::e = B::rrow & 0xFFu;
+                B::tgt = (B::rrow >> 8) & 0xFFu;
+                B::pflags = B::rrow >> 16;
+                B::fr = B::rinit;
+                B::w = 0;
+                if constexpr (TB) {
+                    B::sp = col_addr;
+                    B::set_bks(col_addr);
+                    B::bias = 0;
+                } else {
+                    B::len = 1;
+                }
+                B::step = -1;
+                B::lv = kHwReset;
+                B::rrow = nx.x;
+                B::rinit = ((uint64_t)nx.z << 32) | nx.y;
+                B::rpid = nx.w;
+            }
         } else if constexpr (MV == 3) {
             const bool rs = (B::pending != 0u) & (p.autoreset == 1);
             const uint4 nx = mrow[B::rpid];
@@ -124,11 +167,14 @@ extern "C" int sparc_diag_rollout1s(void* ctx, int32_t T, const uint8_t* d_act, 
             constexpr int MV = decltype(mvc)::value;
             if (g == 1) go(k_rollout1s_diag<TB, false, true, 1, MV>);
             else if (g == 2) go(k_rollout1s_diag<TB, false, true, 2, MV>);
+            else if (g == 3) go(k_rollout1s_diag<TB, false, true, 3, MV>);
             else go(k_rollout1s_diag<TB, false, true, 0, MV>);
         };
         if (mv == 1) pg(std::integral_constant<int, 1>{});
         else if (mv == 2) pg(std::integral_constant<int, 2>{});
         else if (mv == 3) pg(std::integral_constant<int, 3>{});
+        else if (mv == 4) pg(std::integral_constant<int, 4>{});
+        else if (mv == 5) pg(std::integral_constant<int, 5>{});
         else pg(std::integral_constant<int, 0>{});
     };
     if (c->cfg.traceback) pick(std::true_type{});

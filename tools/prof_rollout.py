@@ -30,11 +30,12 @@ ap.add_argument("--rand", action="store_true", help="in-kernel counter-based act
 ap.add_argument("--no-out", action="store_true", help="do not write reward codes / flags")
 ap.add_argument("--time", action="store_true", help="print the mean launch time (HIP events)")
 ap.add_argument("--lib", default=None, help="path of a diagnostic build of libsparc_gym_amd.so")
+ap.add_argument("--rules", action="store_true", help="the rule audit after every step (rollout(rules=True))")
 a = ap.parse_args()
 sizes, full, tb, obs = bench.CONFIGS[a.config]
 proc = process_puzzles(synthetic.make_puzzles(1024, seed=0, sizes=sizes, full_properties=full))
 table = pack_table(proc)
-vec = SPaRCVecEnv(a.envs, processed=proc, table=table, traceback=tb, observation="compact")
+vec = SPaRCVecEnv(a.envs, processed=proc, table=table, traceback=tb, observation="compact", rules=a.rules)
 gid = np.arange(a.envs, dtype=np.uint64)
 vec.reset(options={"puzzle_index": (gid * 2654435761 % len(proc)).astype(np.int64)})
 acts = torch.randint(0, 4, (a.launches + 1, a.chunk, a.envs), dtype=torch.uint8, device="cuda")
@@ -49,7 +50,9 @@ ms = []
 for k in range(a.launches + 1):      # first launch = warmup
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    if a.no_out:
+    if a.rules:
+        vec.rollout(a.chunk, None if a.rand else acts[k], stats=stats, seed=k, rules=True)
+    elif a.no_out:
         vec.rollout(a.chunk, None if a.rand else acts[k], stats=stats, record=False, seed=k)
     else:
         vec.rollout(a.chunk, None if a.rand else acts[k], stats=stats, out=(rew, flg), seed=k,
