@@ -279,6 +279,7 @@ struct ObsTrace {
 struct RuleTrace {
     RulesTab rt;
     uint16_t* bits;
+    FitMemo<kMemo>* memo;   // [N] per-env exact-fit memo, carried between launches (may be null)
 };
 template <int W, bool TB, bool RAND, bool LDS_TABLE, int EPW, bool OBS = false, bool RULES = false>
 __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const uint8_t* __restrict__ act,
@@ -355,8 +356,11 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
                         ot.aout ? ot.aout + run : nullptr);
         }
     };
-    // exact-fit answers of this lane's recent regions (the path moves one point per step)
-    FitMemo<4> memo;
+    // exact-fit answers of this lane's recent regions (the path moves one point per step),
+    // carried between launches and audit calls in HBM
+    FitMemo<kMemo> memo;
+    if constexpr (RULES)
+        if (rtr.memo && i < p.n) memo = rtr.memo[i];
     auto audit_step = [&](int32_t t) {               // rule bits of the state after step t
         if constexpr (RULES) {
             uint64_t v[W];
@@ -437,6 +441,8 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
     }
     if (!active) return;
     e.store(p, src, i);
+    if constexpr (RULES)
+        if (rtr.memo) rtr.memo[i] = memo;
     if (stats) {
         int4 s = stats[i];
         s.x += acc.x;
@@ -1000,7 +1006,8 @@ __global__ void __launch_bounds__(kBlock) k_obs_pack(Params p, int32_t* __restri
 
 template <int W>
 __global__ void __launch_bounds__(kBlock) k_rules(Params p, RulesTab rt, uint16_t* __restrict__ bits,
-                                                  uint8_t* __restrict__ region, uint64_t* __restrict__ fit) {
+                                                  uint8_t* __restrict__ region, uint64_t* __restrict__ fit,
+                                                  FitMemo<kMemo>* __restrict__ memos) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= p.n) return;
     const uint32_t q = p.st.pid[i];
@@ -1014,7 +1021,11 @@ __global__ void __launch_bounds__(kBlock) k_rules(Params p, RulesTab rt, uint16_
     uint8_t* ro = region ? region + (size_t)i * 64 * W : nullptr;
     if (ro)
         for (int k = 0; k < 64 * W; ++k) ro[k] = 0xFF;
-    const RuleOut<W> r = audit<W>(p, rt, vis, ps & 0xFFu, (ps >> 8) & 0xFFu, q, ro);
+    // the env's exact-fit memo: the reference audits every step() (SPaRC_Gym.py:1227), and
+    // consecutive states share most regions
+    FitMemo<kMemo> memo = memos[i];
+    const RuleOut<W> r = audit<W>(p, rt, vis, ps & 0xFFu, (ps >> 8) & 0xFFu, q, ro, &memo);
+    memos[i] = memo;
     if (bits) bits[i] = (uint16_t)r.bits;
     if (fit) fit[i] = r.fit_ok;
 }
@@ -1054,6 +1065,7 @@ struct Ctx {
     uint32_t *r_inst_range = nullptr, *r_inst = nullptr, *r_shape_range = nullptr;
     int32_t* r_shape_area = nullptr;
     int8_t* r_shape_off = nullptr;
+    FitMemo<kMemo>* r_memo = nullptr;   // [N] per-env exact-fit memo of the audit (zeroed at sparc_load_rules)
     uint16_t* s_bits = nullptr;
     uint8_t* s_region = nullptr;
     uint64_t* s_fit = nullptr;
@@ -1228,7 +1240,7 @@ int sparc_destroy(void* ctx) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->vis, c->dirs, c->pos, c->aux, c->step, c->pid, c->t_open, c->t_info, c->t_root, c->t_trie, c->t_trie1, c->t_init, c->t_row1,
                     c->t_trie8, c->t_trow, c->t_mrow, c->t_mroww, c->t_boardw, c->err, c->s_act, c->s_flags, c->s_mask, c->s_rew, c->s_pidx, c->r_planes, c->r_inst_range,
-                    c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off, c->s_bits, c->s_region, c->s_fit};
+                    c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off, c->r_memo, c->s_bits, c->s_region, c->s_fit};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->own) (void)hipStreamDestroy(c->own);
@@ -1594,7 +1606,7 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
     if ((uint64_t)T * c->n > (1ull << 40)) return fail(c, SPARC_E_INVALID, "T*N too large");
     const Params p = make_params(c);
     const ObsTrace no_obs{nullptr, nullptr, 1u, 1u};
-    const RuleTrace no_rules{RulesTab{}, nullptr};
+    const RuleTrace no_rules{RulesTab{}, nullptr, nullptr};
     int lds_rc = SPARC_OK;   // allow_big_lds failure inside a launch lambda (then no launch)
     int4* st = reinterpret_cast<int4*>(d_stats);
     auto aligned = [](const void* q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & 15u) == 0; };
@@ -1777,7 +1789,7 @@ int sparc_rollout_rules_device(void* ctx, int32_t T, const uint8_t* d_act, uint6
     if (!d_rule_bits) return fail(c, SPARC_E_INVALID, "null rule_bits");
     const RuleTrace rtr{RulesTab{c->r_planes, c->r_inst_range, c->r_inst, c->r_shape_range, c->r_shape_area,
                                  c->r_shape_off, c->num_puzzles},
-                        d_rule_bits};
+                        d_rule_bits, c->r_memo};
     return rollout_impl(c, T, d_act, seed, t0, d_rew, d_flags, d_stats, nullptr, &rtr);
 }
 
@@ -1908,6 +1920,9 @@ int sparc_load_rules(void* ctx, const sparc_rules_table* t) {
         HIPCHK(c, hipMemcpy(c->r_shape_area, t->shape_area, sizeof(int32_t) * t->num_shapes, hipMemcpyHostToDevice));
     }
     if (t->num_offsets) HIPCHK(c, hipMemcpy(c->r_shape_off, t->shape_off, 2 * (size_t)t->num_offsets, hipMemcpyHostToDevice));
+    // the memo's entries name puzzles of the old table: start empty (a zero key matches no region)
+    if (!c->r_memo) HIPCHK(c, hipMalloc(&c->r_memo, sizeof(FitMemo<kMemo>) * (size_t)c->n));
+    HIPCHK(c, hipMemset(c->r_memo, 0, sizeof(FitMemo<kMemo>) * (size_t)c->n));
     c->rules = true;
     return SPARC_OK;
 }
@@ -1922,9 +1937,9 @@ int sparc_rules_device(void* ctx, uint16_t* d_bits, uint8_t* d_region, uint64_t*
     const RulesTab rt{c->r_planes, c->r_inst_range, c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off,
                       c->num_puzzles};
     const dim3 g = grid_for(c->n);
-    if (c->W == 1) k_rules<1><<<g, kBlock, 0, c->stream>>>(p, rt, d_bits, d_region, d_fit);
-    else if (c->W == 2) k_rules<2><<<g, kBlock, 0, c->stream>>>(p, rt, d_bits, d_region, d_fit);
-    else k_rules<4><<<g, kBlock, 0, c->stream>>>(p, rt, d_bits, d_region, d_fit);
+    if (c->W == 1) k_rules<1><<<g, kBlock, 0, c->stream>>>(p, rt, d_bits, d_region, d_fit, c->r_memo);
+    else if (c->W == 2) k_rules<2><<<g, kBlock, 0, c->stream>>>(p, rt, d_bits, d_region, d_fit, c->r_memo);
+    else k_rules<4><<<g, kBlock, 0, c->stream>>>(p, rt, d_bits, d_region, d_fit, c->r_memo);
     return launch_check(c);
 }
 

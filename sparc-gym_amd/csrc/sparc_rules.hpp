@@ -257,11 +257,12 @@ __device__ __noinline__ int exact_fit(const FitIn& in, const BB<W>& Rc, uint64_t
 // depends only on the puzzle and the region's cells, and one step moves the path by one point,
 // so most regions (and their fit answers) carry over from the previous steps.  K entries of
 // (cell mask, answer) for one puzzle, replaced round robin; a miss runs the search.
+// All-zero bytes are an empty memo (HBM copies are zeroed): a zero key matches no region.
 template <int K>
 struct FitMemo {
     uint64_t key[K];
-    uint32_t res = 0, pid = ~0u, next = 0;
-    __device__ __forceinline__ FitMemo() {
+    uint32_t res, pid, next, pad;
+    __device__ __forceinline__ FitMemo() : res(0), pid(0), next(0), pad(0) {
 #pragma unroll
         for (int k = 0; k < K; ++k) key[k] = 0;   // a region holds cells: its mask is never 0
     }
@@ -289,6 +290,7 @@ struct FitMemo {
     }
 };
 struct NoMemo {};
+constexpr int kMemo = 4;   // memo entries per env
 
 // ---------------------------------------------------------------- the audit
 template <int W>

@@ -33,6 +33,7 @@ ap.add_argument("--lib", default=None, help="path of a diagnostic build of libsp
 ap.add_argument("--rules", action="store_true", help="the rule audit after every step (rollout(rules=True))")
 a = ap.parse_args()
 sizes, full, tb, obs = bench.CONFIGS[a.config]
+a.rules = a.rules or a.config in bench.RULE_CONFIGS
 proc = process_puzzles(synthetic.make_puzzles(1024, seed=0, sizes=sizes, full_properties=full))
 table = pack_table(proc)
 vec = SPaRCVecEnv(a.envs, processed=proc, table=table, traceback=tb, observation="compact", rules=a.rules)
