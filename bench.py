@@ -119,10 +119,18 @@ def cpu_baseline_rules(proc, tb, max_steps, seconds):
             env.p = pool[q]
             env.reset()
     dt = time.perf_counter() - t1
-    return {"value": round(k / dt, 1), "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/cpu_ref.py step() + oracle/rules_ref.py rule audit once per step (pure Python, the "
-                      f"reference's algorithms), 1 env, {k} steps, random actions, {dt:.1f} s, 1 thread; CPU "
-                      f"{platform.processor() or platform.machine()}, os.cpu_count()={os.cpu_count()}"}
+    out = {"value": round(k / dt, 1), "unit": "env-steps/s", "cores": 1, "kind": "port",
+           "sample": f"oracle/cpu_ref.py step() + oracle/rules_ref.py rule audit once per step (pure Python, the "
+                     f"reference's algorithms), 1 env, {k} steps, random actions, {dt:.1f} s, 1 thread; CPU "
+                     f"{platform.processor() or platform.machine()}, os.cpu_count()={os.cpu_count()}",
+           "value_1core": round(k / dt, 1)}
+    # the same on one process per core of this GPU's share of the host (BASELINE.md's plan)
+    mp_ = _cpu_bench_multi("c3r", "py_rules", max_steps, seconds)
+    if mp_:
+        out.update(value=mp_["value"], cores=mp_["procs"],
+                   sample=out["sample"] + f"; value: {mp_['procs']} processes x 1 env, {mp_['seconds']:.0f} s "
+                                          f"(oracle/cpu_bench.py --impl py_rules)")
+    return out
 
 
 def cpu_baseline(proc, tb, max_steps, seconds, obs_dims=None, config="c3"):
@@ -188,7 +196,24 @@ def cpu_baseline(proc, tb, max_steps, seconds, obs_dims=None, config="c3"):
             out["whole_host_estimate"] = round(mc["value"] / mc["procs"] * phys, 1)
     except (subprocess.SubprocessError, ValueError, KeyError, IndexError) as exc:   # keep the 1-core number
         out["multi_core_error"] = repr(exc)[:200]
+    if not obs_dims:   # the pure-Python port on the same cores (one process per core)
+        mp_ = _cpu_bench_multi(config, "py", max_steps, seconds)
+        if mp_:
+            out["python_port_multicore"] = {"value": mp_["value"], "procs": mp_["procs"],
+                                            "sample": f"oracle/cpu_ref.py, {mp_['procs']} processes x 1 env, "
+                                                      f"{mp_['seconds']:.0f} s (oracle/cpu_bench.py --impl py)"}
     return out
+
+
+def _cpu_bench_multi(config, impl, max_steps, seconds):
+    """oracle/cpu_bench.py in a child process (never touches the GPU); its JSON or None."""
+    cmd = [sys.executable, "-m", "oracle.cpu_bench", "--config", config, "--seconds", str(seconds),
+           "--max-steps", str(max_steps), "--impl", impl]
+    try:
+        r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=seconds * 4 + 120)
+        return json.loads(r.stdout.strip().splitlines()[-1])
+    except (subprocess.SubprocessError, ValueError, IndexError):
+        return None
 
 
 def csrc_hash():

@@ -4,12 +4,16 @@ as a child process (it never touches the GPU) and reports its aggregate rate nex
 single-thread one, as BASELINE.md's CPU-baseline plan asks (one process per host core, core
 count stated).
 
-    python -m oracle.cpu_bench --config c3 --procs 16 --seconds 10 [--obs X Y]
+    python -m oracle.cpu_bench --config c3 --procs 16 --seconds 10 [--obs X Y] [--impl c|py|py_rules]
 
 Each process runs 1,024 envs of the bench pool (synthetic seed 0, the same puzzle assignment as
 bench.py) with counter-based random actions and next-step autoreset, for `seconds`; with
 --obs it also writes the visited / agent_location planes of every step (config c4).  Prints
 one JSON line: {"value": env-steps/s summed over processes, "procs": P, ...}.
+
+--impl py runs the pure-Python restatement instead (oracle/cpu_ref.py: the reference's step()
+core at reference speed, one env at a time), --impl py_rules the same plus the rule audit of
+oracle/rules_ref.py once per step (the reference's full step(): _validate_rules, 941-950).
 """
 from __future__ import annotations
 
@@ -27,8 +31,17 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CONFIGS = {   # name: (grid sizes, full property set, traceback) — as bench.CONFIGS
     "c2": (((3, 3),), False, False),
     "c3": (((3, 3),), True, True),
+    "c3r": (((3, 3),), True, True),
     "c4": (((2, 2), (3, 3), (4, 4), (5, 5)), True, True),
 }
+
+
+def make_proc(config, n_puzzles):
+    sys.path.insert(0, os.path.join(REPO, "sparc-gym_amd"))
+    from sparc_gym_amd import synthetic                      # host-side only: no HIP library
+    from sparc_gym_amd.puzzles import process_puzzles
+    sizes, full, _ = CONFIGS[config]
+    return process_puzzles(synthetic.make_puzzles(n_puzzles, seed=0, sizes=sizes, full_properties=full))
 
 
 def make_pool(config, n_puzzles):
@@ -60,6 +73,30 @@ def _worker(args):
     return n * steps, time.perf_counter() - t0
 
 
+def _worker_py(args):
+    """One env at a time through oracle/cpu_ref.py (+ oracle/rules_ref.py's audit per step)."""
+    proc, tb, max_steps, seconds, rules, rank = args
+    from oracle.cpu_ref import CpuRefEnv
+    from oracle import rules_ref
+    pool = [{"x_size": p["x_size"], "y_size": p["y_size"], "start": list(p["start_location"]),
+             "target": list(p["target_location"]), "solution_count": p["solution_count"],
+             "solution_paths": p["solution_paths"], "gaps": p["obs_array"]["gaps"]} for p in proc]
+    rng = np.random.default_rng(rank)
+    q = (rank * 2654435761) % len(pool)
+    env = CpuRefEnv(pool[q], tb, max_steps)
+    k, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        _, term, trunc = env.step(int(rng.integers(4)))
+        if rules:
+            rules_ref.audit(proc[q], env.path, env.loc, term, trunc)
+        k += 1
+        if term or trunc:
+            q = (q + 1) % len(pool)
+            env.p = pool[q]
+            env.reset()
+    return k, time.perf_counter() - t0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
@@ -68,19 +105,26 @@ def main():
     ap.add_argument("--puzzles", type=int, default=1024)
     ap.add_argument("--max-steps", type=int, default=2000)
     ap.add_argument("--obs", type=int, nargs=2, default=None, metavar=("X", "Y"))
+    ap.add_argument("--impl", default="c", choices=["c", "py", "py_rules"])
     a = ap.parse_args()
     usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     procs = a.procs if a.procs > 0 else max(1, min(16, usable))
-    pool = make_pool(a.config, a.puzzles)
-    from oracle import build
-    build()                                                      # compile once, before forking
     tb = CONFIGS[a.config][2]
-    with mp.get_context("fork").Pool(procs) as p:
-        res = p.map(_worker, [(pool, tb, a.max_steps, a.seconds, a.obs, r) for r in range(procs)])
+    if a.impl == "c":
+        pool = make_pool(a.config, a.puzzles)
+        from oracle import build
+        build()                                                  # compile once, before forking
+        with mp.get_context("fork").Pool(procs) as p:
+            res = p.map(_worker, [(pool, tb, a.max_steps, a.seconds, a.obs, r) for r in range(procs)])
+    else:
+        proc = make_proc(a.config, a.puzzles)
+        with mp.get_context("fork").Pool(procs) as p:
+            res = p.map(_worker_py, [(proc, tb, a.max_steps, a.seconds, a.impl == "py_rules", r)
+                                     for r in range(procs)])
     value = sum(s / dt for s, dt in res)
     print(json.dumps({"value": round(value, 1), "procs": procs, "usable_cores": usable,
                       "os_cpu_count": os.cpu_count(), "config": a.config, "seconds": a.seconds,
-                      "env_steps": int(sum(s for s, _ in res)), "obs": a.obs}))
+                      "env_steps": int(sum(s for s, _ in res)), "obs": a.obs, "impl": a.impl}))
 
 
 if __name__ == "__main__":
