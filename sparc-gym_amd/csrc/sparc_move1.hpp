@@ -67,7 +67,6 @@ struct MoveLane1 {
     uint32_t lv = 0x30000u;               // flag-bit mask of the step: term | trunc, or kHwReset
     uint32_t rpid = 0, rrow = 0;          // the next autoreset's row word and the puzzle after it
     uint64_t rinit = 0;                   // ... and its free board
-    uint4 nx = {0u, 0u, 0u, 0u};          // mrow[rpid]: the row of the autoreset after the next
 
     typedef __attribute__((address_space(3))) uint8_t lds_u8;
     __device__ __forceinline__ static lds_u8* lds_byte(uint32_t a) { return (lds_u8*)(uintptr_t)a; }
@@ -82,16 +81,17 @@ struct MoveLane1 {
         rrow = m.x;
         rinit = ((uint64_t)m.z << 32) | m.y;
         rpid = m.w;
-        nx = mrow[rpid];
     }
 
     // gymnasium next-step autoreset (reset(), SPaRC_Gym.py:1087): the next puzzle's row and
-    // board from registers; the step then moves nowhere (w = 0, bias = 0) and reports the reset
-    // flag instead of term / trunc (lv).  The row of the reset after it (nx) was read a step
-    // ago, and the next one is read after the branch, on every step: read inside, the branch
-    // waits for it (it lands in temporaries and is copied on), and about a fifth of all
-    // wave-steps take the branch (MI355X, per-role stamps of tools/diag_split.py)
+    // board from registers (read at the previous reset); the step then moves nowhere (w = 0,
+    // bias = 0) and reports the reset flag instead of term / trunc (lv).  The row of the reset
+    // after it is read on every step, outside the branch: read inside, the branch waits for it
+    // (it lands in temporaries and is copied on), and about a fifth of all wave-steps take the
+    // branch (MI355X, per-role stamps of tools/diag_split.py: the move wave's step 421.8 ->
+    // 409.3 cycles at 65,536 envs)
     __device__ __forceinline__ void reset_next(const Params& p, const uint4* mrow, uint32_t col_addr) {
+        const uint4 nx = mrow[rpid];
         if ((pending != 0u) & (p.autoreset == 1)) {
             e = rrow & 0xFFu;
             tgt = (rrow >> 8) & 0xFFu;
@@ -111,7 +111,6 @@ struct MoveLane1 {
             rinit = ((uint64_t)nx.z << 32) | nx.y;
             rpid = nx.w;
         }
-        nx = mrow[rpid];
     }
 
     // one env-step's move part (1131-1199) from the target's window position; returns the
