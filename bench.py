@@ -442,7 +442,7 @@ def main():
     # algorithmic HBM bytes per launch: per env-step action 1 + reward 1 + flags 1; per env and
     # launch the state (load + store) and, for rollouts, the stats record (load + store)
     sb = state_bytes_per_env(table.words, tb)
-    per_env_launch = 2 * sb + (32 if args.mode == "rollout" else 0)
+    per_env_launch = 2 * sb + (32 if args.mode == "rollout" else 0) + (96 if rules else 0)
     per_step = 3 + (2 * plane_bytes if obs and args.mode == "rollout" else 0) + (2 if rules else 0)
     bytes_launch = n * (per_step * avg_T + per_env_launch)
     achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
@@ -520,7 +520,8 @@ def main():
                                     f"{', rule bits 2 B' if rules else ''}"
                                     f"); per env per launch "
                                     f"{per_env_launch} B (state {sb} B load+store"
-                                    f"{', stats 16 B load+store' if args.mode == 'rollout' else ''})"},
+                                    f"{', stats 16 B load+store' if args.mode == 'rollout' else ''}"
+                                    f"{', exact-fit memo 48 B load+store' if rules else ''})"},
         "episodes": summary,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and rules:
