@@ -33,6 +33,8 @@ CONFIGS = {   # name: (grid sizes, full property set, traceback) — as bench.CO
     "c3": (((3, 3),), True, True),
     "c3r": (((3, 3),), True, True),
     "c4": (((2, 2), (3, 3), (4, 4), (5, 5)), True, True),
+    "c4c": (((2, 2), (3, 3), (4, 4), (5, 5)), True, True),
+    "c3g7": (((7, 7),), True, True),
 }
 
 

@@ -62,3 +62,11 @@ def test_world_mismatch_refused(monkeypatch):
     with pytest.raises(SystemExit) as e:
         bench.main()
     assert "WORLD_SIZE=2" in str(e.value)
+
+
+def test_cpu_bench_covers_every_bench_config():
+    """The multi-core CPU baseline (oracle/cpu_bench.py, run by bench's cpu_baseline leg) knows
+    every bench workload with the same lattices, property set and traceback flag."""
+    from oracle import cpu_bench
+    for name, (sizes, full, tb, _obs) in bench.CONFIGS.items():
+        assert cpu_bench.CONFIGS[name] == (sizes, full, tb), name
