@@ -287,7 +287,7 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
                                                     uint8_t* __restrict__ flg, int4* __restrict__ stats,
                                                     uint32_t tiled, ObsTrace ot, RuleTrace rtr) {
     static_assert(!OBS || EPW == 64, "the observation writer needs full 64-lane waves");
-    constexpr int kUnrollSteps = OBS ? 1 : 4;   // OBS: one step body (its plane writer is long)
+    constexpr int kUnrollSteps = (OBS || RULES) ? 1 : 4;   // OBS / RULES: one step body (the plane writer / audit is long)
     // LDS: [I/O tiles, 3*16*EPW B per wave][W=1 traceback: move stacks, 64*EPW B per wave][rows]
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -375,11 +375,11 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
         }
     };
     u32x4 anext = {0u, 0u, 0u, 0u};
-    if (!RAND && !RULES && full && T >= kTile) anext = nt_load16(act + (size_t)r * n + wave_base + c);
+    if (!RAND && full && T >= kTile) anext = nt_load16(act + (size_t)r * n + wave_base + c);
 
     for (int32_t tb = 0; tb < T; tb += kTile) {
         const int32_t cnt = T - tb < kTile ? T - tb : kTile;
-        if (!RULES && full && cnt == kTile) {
+        if (full && cnt == kTile) {
             if constexpr (!RAND) {
                 const u32x4 acur = anext;
                 if (tb + 2 * kTile <= T) anext = nt_load16(act + (size_t)(tb + kTile + r) * n + wave_base + c);
@@ -400,6 +400,7 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
                     uint32_t f;
                     const int code = e.advance(p, src, av[j], f);
                     obs(tb + k);
+                    audit_step(tb + k);
                     tr[k * EPW + lane] = (uint8_t)code;
                     tf[k * EPW + lane] = (uint8_t)f;
                     if constexpr (W == 1) {   // per-step flags the W = 1 step already has
@@ -1030,6 +1031,16 @@ __global__ void __launch_bounds__(kBlock) k_rules(Params p, RulesTab rt, uint16_
     if (fit) fit[i] = r.fit_ok;
 }
 
+// the exact-fit answer table (sparc_rules.hpp fit_table_word): one word per (puzzle, mask group)
+template <int W>
+__global__ void __launch_bounds__(kBlock) k_fit_table(Params p, RulesTab rt, const uint2* __restrict__ items,
+                                                      uint32_t count, uint32_t* __restrict__ tab) {
+    const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
+    if (k >= count) return;
+    const uint2 it = items[k];
+    tab[rt.fit_off[it.x] / 16u + it.y] = fit_table_word<W>(p, rt, it.x, it.y);
+}
+
 // ------------------------------------------------------------------------------ host side
 struct Ctx {
     sparc_config cfg{};
@@ -1061,11 +1072,13 @@ struct Ctx {
     uint32_t* s_pidx = nullptr;
     // rule table (sparc_load_rules)
     bool rules = false;
-    uint64_t* r_planes = nullptr;
+    uint64_t* r_planes = nullptr;   // [P][RP_COUNT][W] (sparc_rules.hpp: the ABI planes + derived ones)
+    bool r_area = false;
     uint32_t *r_inst_range = nullptr, *r_inst = nullptr, *r_shape_range = nullptr;
     int32_t* r_shape_area = nullptr;
     int8_t* r_shape_off = nullptr;
-    FitMemo<kMemo>* r_memo = nullptr;   // [N] per-env exact-fit memo of the audit (zeroed at sparc_load_rules)
+    FitMemo<kMemo>* r_memo = nullptr;
+    uint32_t *r_fit_off = nullptr, *r_fit_tab = nullptr;   // exact-fit answer table (sparc_rules.hpp)   // [N] per-env exact-fit memo of the audit (zeroed at sparc_load_rules)
     uint16_t* s_bits = nullptr;
     uint8_t* s_region = nullptr;
     uint64_t* s_fit = nullptr;
@@ -1240,7 +1253,7 @@ int sparc_destroy(void* ctx) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->vis, c->dirs, c->pos, c->aux, c->step, c->pid, c->t_open, c->t_info, c->t_root, c->t_trie, c->t_trie1, c->t_init, c->t_row1,
                     c->t_trie8, c->t_trow, c->t_mrow, c->t_mroww, c->t_boardw, c->err, c->s_act, c->s_flags, c->s_mask, c->s_rew, c->s_pidx, c->r_planes, c->r_inst_range,
-                    c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off, c->r_memo, c->s_bits, c->s_region, c->s_fit};
+                    c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off, c->r_memo, c->s_bits, c->s_region, c->s_fit, c->r_fit_off, c->r_fit_tab};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->own) (void)hipStreamDestroy(c->own);
@@ -1788,7 +1801,7 @@ int sparc_rollout_rules_device(void* ctx, int32_t T, const uint8_t* d_act, uint6
     if (!c->rules) return fail(c, SPARC_E_STATE, "sparc_load_rules has not been called");
     if (!d_rule_bits) return fail(c, SPARC_E_INVALID, "null rule_bits");
     const RuleTrace rtr{RulesTab{c->r_planes, c->r_inst_range, c->r_inst, c->r_shape_range, c->r_shape_area,
-                                 c->r_shape_off, c->num_puzzles},
+                                 c->r_shape_off, c->num_puzzles, c->r_area ? 1u : 0u, c->r_fit_off, c->r_fit_tab},
                         d_rule_bits, c->r_memo};
     return rollout_impl(c, T, d_act, seed, t0, d_rew, d_flags, d_stats, nullptr, &rtr);
 }
@@ -1897,13 +1910,38 @@ int sparc_load_rules(void* ctx, const sparc_rules_table* t) {
             return fail(c, SPARC_E_INVALID, m);
         }
     }
-    void* old[] = {c->r_planes, c->r_inst_range, c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off};
+    void* old[] = {c->r_planes, c->r_inst_range, c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off,
+                   c->r_fit_off, c->r_fit_tab};
     for (void* b : old)
         if (b) HIPCHK(c, hipFree(b));
     c->r_planes = nullptr; c->r_inst_range = nullptr; c->r_inst = nullptr;
     c->r_shape_range = nullptr; c->r_shape_area = nullptr; c->r_shape_off = nullptr;
+    c->r_fit_off = nullptr; c->r_fit_tab = nullptr;
     c->rules = false;
+    // the device copy: the caller's SPARC_RULE_PLANES planes per puzzle, RP_INST rewritten from the
+    // instance list, then the bit-sliced net area of each cell (kAreaPlanes planes, sparc_rules.hpp)
+    static_assert(RP_ABI == SPARC_RULE_PLANES, "rule plane layout");
     const size_t np_ = P * RP_COUNT * W;
+    std::vector<uint64_t> dev_planes(np_, 0ull);
+    bool area_ok = true;
+    for (size_t q = 0; q < P; ++q) {
+        uint64_t* d = dev_planes.data() + q * RP_COUNT * W;
+        std::copy(t->planes + q * RP_ABI * W, t->planes + (q + 1) * RP_ABI * W, d);
+        for (int k = 0; k < W; ++k) d[RP_INST * W + k] = 0;
+        int32_t net[256] = {0};
+        const uint32_t f = t->inst_range[q] & 0xFFFFu, n = t->inst_range[q] >> 16;
+        for (uint32_t k = 0; k < n; ++k) {
+            const uint32_t e = t->inst[f + k], b = e & 0x3FFu;
+            const int64_t a = t->shape_area[e >> 17];
+            net[b] = (int32_t)std::max<int64_t>(-(1 << 20), std::min<int64_t>(1 << 20, net[b] + (((e >> 10) & 1u) ? -a : a)));
+            d[RP_INST * W + (b >> 6)] |= 1ull << (b & 63);
+        }
+        for (uint32_t b = 0; b < 64u * W; ++b) {
+            if (net[b] < -(1 << (kAreaPlanes - 1)) || net[b] >= (1 << (kAreaPlanes - 1))) area_ok = false;
+            for (int k = 0; k < kAreaPlanes; ++k)
+                if (((uint32_t)net[b] >> k) & 1u) d[(RP_AREA0 + k) * W + (b >> 6)] |= 1ull << (b & 63);
+        }
+    }
     const size_t ni = std::max<size_t>(1, t->num_inst), ns = std::max<size_t>(1, t->num_shapes),
                  no = std::max<size_t>(1, t->num_offsets);
     HIPCHK(c, hipMalloc(&c->r_planes, sizeof(uint64_t) * np_));
@@ -1912,7 +1950,8 @@ int sparc_load_rules(void* ctx, const sparc_rules_table* t) {
     HIPCHK(c, hipMalloc(&c->r_shape_range, sizeof(uint32_t) * ns));
     HIPCHK(c, hipMalloc(&c->r_shape_area, sizeof(int32_t) * ns));
     HIPCHK(c, hipMalloc(&c->r_shape_off, 2 * no));
-    HIPCHK(c, hipMemcpy(c->r_planes, t->planes, sizeof(uint64_t) * np_, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->r_planes, dev_planes.data(), sizeof(uint64_t) * np_, hipMemcpyHostToDevice));
+    c->r_area = area_ok;   // a cell's net area outside -128..127: the audit walks the list instead
     HIPCHK(c, hipMemcpy(c->r_inst_range, t->inst_range, sizeof(uint32_t) * P, hipMemcpyHostToDevice));
     if (t->num_inst) HIPCHK(c, hipMemcpy(c->r_inst, t->inst, sizeof(uint32_t) * t->num_inst, hipMemcpyHostToDevice));
     if (t->num_shapes) {
@@ -1923,6 +1962,41 @@ int sparc_load_rules(void* ctx, const sparc_rules_table* t) {
     // the memo's entries name puzzles of the old table: start empty (a zero key matches no region)
     if (!c->r_memo) HIPCHK(c, hipMalloc(&c->r_memo, sizeof(FitMemo<kMemo>) * (size_t)c->n));
     HIPCHK(c, hipMemset(c->r_memo, 0, sizeof(FitMemo<kMemo>) * (size_t)c->n));
+    // the exact-fit answer of every region cell mask of each puzzle with at most kFitTabCells
+    // cells, computed once here by the audit's own search (k_fit_table): the audit then looks
+    // answers up instead of searching (the memo serves the larger puzzles)
+    std::vector<uint32_t> fit_off(P, kNoFitTab);
+    std::vector<uint2> items;
+    size_t entries = 0;
+    for (size_t q = 0; q < P; ++q) {
+        const uint32_t X = info[q].x & 0xFFu, Y = (info[q].x >> 8) & 0xFFu;
+        const uint32_t cells = ((X - 1) / 2) * ((Y - 1) / 2);
+        if (cells > kFitTabCells || (t->inst_range[q] >> 16) == 0) continue;
+        const uint32_t words = cells <= 4 ? 1u : 1u << (cells - 4);
+        fit_off[q] = (uint32_t)entries;
+        for (uint32_t g = 0; g < words; ++g) items.push_back(make_uint2((uint32_t)q, g));
+        entries += 16u * words;
+    }
+    if (!items.empty()) {
+        const size_t words = entries / 16;
+        uint2* d_items = nullptr;
+        HIPCHK(c, hipMalloc(&c->r_fit_off, sizeof(uint32_t) * P));
+        HIPCHK(c, hipMalloc(&c->r_fit_tab, sizeof(uint32_t) * words));
+        HIPCHK(c, hipMalloc(&d_items, sizeof(uint2) * items.size()));
+        HIPCHK(c, hipMemcpy(c->r_fit_off, fit_off.data(), sizeof(uint32_t) * P, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(d_items, items.data(), sizeof(uint2) * items.size(), hipMemcpyHostToDevice));
+        const Params p = make_params(c);
+        const RulesTab rt{c->r_planes, c->r_inst_range, c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off,
+                          c->num_puzzles, c->r_area ? 1u : 0u, c->r_fit_off, nullptr};
+        const dim3 g((unsigned)((items.size() + kBlock - 1) / kBlock));
+        if (W == 1) k_fit_table<1><<<g, kBlock, 0, c->stream>>>(p, rt, d_items, (uint32_t)items.size(), c->r_fit_tab);
+        else if (W == 2) k_fit_table<2><<<g, kBlock, 0, c->stream>>>(p, rt, d_items, (uint32_t)items.size(), c->r_fit_tab);
+        else k_fit_table<4><<<g, kBlock, 0, c->stream>>>(p, rt, d_items, (uint32_t)items.size(), c->r_fit_tab);
+        rc = launch_check(c);
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, hipFree(d_items));
+        if (rc) return rc;
+    }
     c->rules = true;
     return SPARC_OK;
 }
@@ -1935,7 +2009,7 @@ int sparc_rules_device(void* ctx, uint16_t* d_bits, uint8_t* d_region, uint64_t*
     if (!c->rules) return fail(c, SPARC_E_STATE, "sparc_load_rules has not been called");
     const Params p = make_params(c);
     const RulesTab rt{c->r_planes, c->r_inst_range, c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off,
-                      c->num_puzzles};
+                      c->num_puzzles, c->r_area ? 1u : 0u, c->r_fit_off, c->r_fit_tab};
     const dim3 g = grid_for(c->n);
     if (c->W == 1) k_rules<1><<<g, kBlock, 0, c->stream>>>(p, rt, d_bits, d_region, d_fit, c->r_memo);
     else if (c->W == 2) k_rules<2><<<g, kBlock, 0, c->stream>>>(p, rt, d_bits, d_region, d_fit, c->r_memo);

@@ -35,11 +35,18 @@
 namespace sparc {
 
 constexpr uint32_t kErrRuleTable = 8;
-// rule-plane indices of include/sparc_gym_amd.h (SPARC_RULE_PLANES)
+// rule-plane indices of include/sparc_gym_amd.h (SPARC_RULE_PLANES), then the planes the loader
+// (sparc_load_rules) derives from the instance list for the device copy: the net instance area
+// of each cell (Σ poly areas − Σ ylop areas of the instances there, 8-bit two's complement,
+// bit-sliced), so a region's area check (_polyfit_check_area 700-709) is 8 popcounts instead of
+// a walk over the puzzle's instance list with two dependent loads per instance.  RP_INST of the
+// device copy is rewritten from the list too (cells holding an instance).
 enum : uint32_t {
     RP_CELLS = 0, RP_LATTICE, RP_GAPS, RP_DOTS, RP_TRI, RP_TRI0, RP_TRI1, RP_TRI2, RP_STAR, RP_SQUARE,
-    RP_COLORED, RP_COL1, RP_M0 = RP_COL1 + 8, RP_M1, RP_M2, RP_NOTFIRST, RP_NOTLAST, RP_INST, RP_COUNT
+    RP_COLORED, RP_COL1, RP_M0 = RP_COL1 + 8, RP_M1, RP_M2, RP_NOTFIRST, RP_NOTLAST, RP_INST, RP_ABI,
+    RP_AREA0 = RP_ABI, RP_COUNT = RP_AREA0 + 8
 };
+constexpr int kAreaPlanes = 8;
 constexpr int kFitCells = 64;     // cell grid of the exact fit (15 x 15 lattice: 7 x 7 = 49)
 constexpr int kFitYlops = 16;     // per puzzle limits, validated by the loader
 constexpr int kFitShapes = 16;
@@ -54,7 +61,16 @@ struct RulesTab {
     const int32_t* __restrict__ shape_area;   // [S] sum of the shape array (the area of 722-723)
     const int8_t* __restrict__ shape_off;     // [offsets][2] (dcx, dcy) in cell units
     uint32_t num_puzzles;
+    uint32_t area;   // 1: the RP_AREA planes hold every cell's net area (else the list is walked)
+    // exact-fit answers of every region cell mask of the puzzles with at most kFitTabCells cells
+    // (sparc_load_rules runs exact_fit over all of them once): fit_off[q] = the puzzle's first
+    // entry (a multiple of 16) or kNoFitTab; entries of 2 bits, 16 per word of fit_tab:
+    // 0 no fit, 1 fits, 2 search exhausted.  May be null (no table).
+    const uint32_t* __restrict__ fit_off;
+    const uint32_t* __restrict__ fit_tab;
 };
+constexpr uint32_t kNoFitTab = 0xFFFFFFFFu;
+constexpr uint32_t kFitTabCells = 12;
 
 template <int W>
 struct BB {
@@ -292,6 +308,59 @@ struct FitMemo {
 struct NoMemo {};
 constexpr int kMemo = 4;   // memo entries per env
 
+// Σ over the region's instances of (poly area − ylop area), and whether it holds any
+// (_polyfit_check_area 700-709 on the instances of 687-697).  Rc: the region's cell centres.
+template <int W>
+__device__ __forceinline__ bool region_net_area(const RulesTab& rt, const FitIn& fin, uint32_t q, const BB<W>& Rc,
+                                                const BB<W>& inst_plane, int& net) {
+    net = 0;
+    if (!(Rc & inst_plane).any()) return false;               // regions without instances skip this
+    if (rt.area) {                                             // the bit-sliced planes: 8 popcounts
+        const uint64_t* ga = rt.planes + ((size_t)q * RP_COUNT + RP_AREA0) * W;
+        BB<W> ap[kAreaPlanes];
+#pragma unroll
+        for (int k = 0; k < kAreaPlanes; ++k) ap[k] = BB<W>::load(ga + k * W);
+#pragma unroll
+        for (int k = 0; k < kAreaPlanes - 1; ++k) net += (Rc & ap[k]).popc() << k;
+        net -= (Rc & ap[kAreaPlanes - 1]).popc() << (kAreaPlanes - 1);
+        return true;
+    }
+    bool has = false;
+    for (uint32_t k = 0; k < fin.count; ++k) {
+        const uint32_t e = rt.inst[fin.first + k];
+        if (!Rc.test(e & 0x3FFu)) continue;
+        has = true;
+        const int a = rt.shape_area[e >> 17];
+        net += ((e >> 10) & 1u) ? -a : a;
+    }
+    return has;
+}
+
+// One entry word of the fit table: the exact-fit answers of region cell masks 16·g .. 16·g + 15
+// of puzzle q (masks whose area check fails, or with no instance, are never looked up: 0).
+template <int W>
+__device__ uint32_t fit_table_word(const Params& p, const RulesTab& rt, uint32_t q, uint32_t g) {
+    const uint4 inf = p.tab.info[q];
+    const uint32_t X = inf.x & 0xFFu, Y = (inf.x >> 8) & 0xFFu;
+    const uint32_t ir = rt.inst_range[q];
+    const FitIn fin{&rt, ir & 0xFFFFu, ir >> 16, (X - 1) / 2, (Y - 1) / 2};
+    const uint32_t cells = fin.CX * fin.CY;
+    const BB<W> inst_plane = BB<W>::load(rt.planes + ((size_t)q * RP_COUNT + RP_INST) * W);
+    uint32_t word = 0;
+    for (uint32_t j = 0; j < 16; ++j) {
+        const uint32_t m = 16u * g + j;
+        if (m == 0 || m >= (1u << cells)) continue;
+        BB<W> Rc = BB<W>::zero();
+        for (uint32_t b = 0; b < cells; ++b)
+            if ((m >> b) & 1u) Rc.set((2 * (b / fin.CY) + 1) * p.pitch + 2 * (b % fin.CY) + 1);
+        int net;
+        if (!region_net_area<W>(rt, fin, q, Rc, inst_plane, net) || Rc.popc() != net) continue;
+        const int r = exact_fit<W>(fin, Rc, (uint64_t)m);
+        word |= (r < 0 ? 2u : (uint32_t)r) << (2 * j);
+    }
+    return word;
+}
+
 // ---------------------------------------------------------------- the audit
 template <int W>
 struct RuleOut {
@@ -305,11 +374,11 @@ template <int W, class Memo = NoMemo>
 __device__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const BB<W>& vis, uint32_t x, uint32_t y,
                             uint32_t q, uint8_t* region_out, Memo* memo = nullptr) {
     // every plane of the puzzle in registers up front: one round of loads, none in the loops
-    BB<W> pl[RP_COUNT];
+    BB<W> pl[RP_ABI];
     {
         const uint64_t* g = rt.planes + (size_t)q * RP_COUNT * W;
 #pragma unroll
-        for (int k = 0; k < (int)RP_COUNT; ++k) pl[k] = BB<W>::load(g + k * W);
+        for (int k = 0; k < (int)RP_ABI; ++k) pl[k] = BB<W>::load(g + k * W);
     }
     const uint4 inf = p.tab.info[q];
     const uint32_t X = inf.x & 0xFFu, Y = (inf.x >> 8) & 0xFFu;
@@ -322,6 +391,7 @@ __device__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const BB<W>& vi
     const BB<W> allowed = lattice.andnot(gaps | vis) | cells;
     const uint32_t ir = rt.inst_range[q];
     const FitIn fin{&rt, ir & 0xFFFFu, ir >> 16, (X - 1) / 2, (Y - 1) / 2};
+    const uint32_t fo = rt.fit_off ? rt.fit_off[q] : kNoFitTab;
 
     bool sq_ok = true, star_ok = true, poly_ok = true, exhausted = false;
     uint64_t fit_ok = 0;
@@ -368,26 +438,23 @@ __device__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const BB<W>& vi
             }
         }
         // poly / ylop (648-709)
-        int pa = 0, ya = 0;
-        bool has = false;
-        if ((Rc & pl[RP_INST]).any())                          // regions without instances skip the list
-        for (uint32_t k = 0; k < fin.count; ++k) {
-            const uint32_t e = rt.inst[fin.first + k];
-            if (!Rc.test(e & 0x3FFu)) continue;
-            has = true;
-            const int a = rt.shape_area[e >> 17];
-            if ((e >> 10) & 1u) ya += a; else pa += a;
-        }
-        if (has) {
-            bool ok = Rc.popc() == pa - ya;
+        int net;
+        if (region_net_area<W>(rt, fin, q, Rc, pl[RP_INST], net)) {
+            bool ok = Rc.popc() == net;
             if (ok) {
                 const uint64_t rm = cell_mask<W>(fin, Rc, P);
                 int r = -1;
-                if constexpr (!std::is_same<Memo, NoMemo>::value) r = memo->find(q, rm);
-                if (r < 0) {
-                    r = exact_fit<W>(fin, Rc, rm);
-                    if constexpr (!std::is_same<Memo, NoMemo>::value)
-                        if (r >= 0) memo->put(q, rm, r);
+                if (fo != kNoFitTab) {                         // the precomputed answer
+                    const uint32_t m = (uint32_t)rm;
+                    const uint32_t a = (rt.fit_tab[(fo + m) >> 4] >> ((m & 15u) * 2u)) & 3u;
+                    r = a == 2u ? -1 : (int)a;
+                } else {
+                    if constexpr (!std::is_same<Memo, NoMemo>::value) r = memo->find(q, rm);
+                    if (r < 0) {
+                        r = exact_fit<W>(fin, Rc, rm);
+                        if constexpr (!std::is_same<Memo, NoMemo>::value)
+                            if (r >= 0) memo->put(q, rm, r);
+                    }
                 }
                 exhausted |= r < 0;
                 ok = r > 0;

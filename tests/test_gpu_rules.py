@@ -213,3 +213,39 @@ def test_rollout_rules_c3r_full_size(on_gpu):
             want = rules_ref.rule_bits(rules_ref.audit(p, path, (int(st["x"][j]), int(st["y"][j]))))
             assert int(bits[t, i]) & 0x1FF == want, (t, i)
     assert len(np.unique(bits)) > 4
+
+
+def test_rules_area_list_fallback_vs_oracle(on_gpu):
+    """A pool holding a shape of area 144 (a 12 x 12 block: a cell's net instance area outside the
+    loader's 8-bit area planes): sparc_load_rules then leaves the area check to the walk over each
+    region's instance list (sparc_rules.hpp region_net_area); k_rules bits still equal the
+    oracle's (_polyfit_check_area 700-709; the big shape fails every area check, as in the
+    reference)."""
+    from sparc_gym_amd import SPaRCVecEnv, synthetic
+    from sparc_gym_amd.puzzles import process_puzzles
+    proc = process_puzzles(synthetic.make_rule_puzzles(256, seed=8, sizes=((3, 3),), break_prob=0.3))
+    big = 0
+    for p in proc:
+        if isinstance(p["polyshapes"], dict) and p["polyshapes"] and big < 16:
+            name = sorted(p["polyshapes"])[0]
+            p["polyshapes"] = dict(p["polyshapes"])
+            p["polyshapes"][name] = [[1] * 12 for _ in range(12)]
+            big += 1
+    assert big == 16
+    n = 4096
+    vec = SPaRCVecEnv(n, processed=proc, traceback=True, autoreset="next_step", observation="compact",
+                      rules=True)
+    vec.reset(options={"puzzle_index": np.arange(n) % len(proc)})
+    refp = [dict(p) for p in proc]
+    rng = np.random.default_rng(4)
+    for T in (0, 9, 30):
+        if T:
+            vec.rollout(T, None, seed=T, record=False)
+        bits = vec.rule_audit()["bits"].cpu().numpy().astype(np.uint16)
+        st = vec.state()
+        for i in rng.choice(n, size=300, replace=False):
+            p = refp[int(st["puzzle"][i])]
+            path = _state_points(st["visited"][:, i], vec.table.pitch, p["x_size"], p["y_size"])
+            want = rules_ref.rule_bits(rules_ref.audit(p, path, (int(st["x"][i]), int(st["y"][i]))))
+            assert int(bits[i]) == want, (T, i)
+    vec.core.sync()
