@@ -1031,14 +1031,14 @@ __global__ void __launch_bounds__(kBlock) k_rules(Params p, RulesTab rt, uint16_
     if (fit) fit[i] = r.fit_ok;
 }
 
-// the exact-fit answer table (sparc_rules.hpp fit_table_word): one word per (puzzle, mask group)
+// the region-code table (sparc_rules.hpp region_table_word): one word per (puzzle, mask group)
 template <int W>
-__global__ void __launch_bounds__(kBlock) k_fit_table(Params p, RulesTab rt, const uint2* __restrict__ items,
-                                                      uint32_t count, uint32_t* __restrict__ tab) {
+__global__ void __launch_bounds__(kBlock) k_region_table(Params p, RulesTab rt, const uint2* __restrict__ items,
+                                                         uint32_t count, uint32_t* __restrict__ tab) {
     const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
     if (k >= count) return;
     const uint2 it = items[k];
-    tab[rt.fit_off[it.x] / 16u + it.y] = fit_table_word<W>(p, rt, it.x, it.y);
+    tab[rt.reg_off[it.x] / 8u + it.y] = region_table_word<W>(p, rt, it.x, it.y);
 }
 
 // ------------------------------------------------------------------------------ host side
@@ -1077,8 +1077,8 @@ struct Ctx {
     uint32_t *r_inst_range = nullptr, *r_inst = nullptr, *r_shape_range = nullptr;
     int32_t* r_shape_area = nullptr;
     int8_t* r_shape_off = nullptr;
-    FitMemo<kMemo>* r_memo = nullptr;
-    uint32_t *r_fit_off = nullptr, *r_fit_tab = nullptr;   // exact-fit answer table (sparc_rules.hpp)   // [N] per-env exact-fit memo of the audit (zeroed at sparc_load_rules)
+    FitMemo<kMemo>* r_memo = nullptr;   // [N] per-env exact-fit memo of the audit (zeroed at sparc_load_rules)
+    uint32_t *r_reg_off = nullptr, *r_reg_tab = nullptr;   // region-code table (sparc_rules.hpp)
     uint16_t* s_bits = nullptr;
     uint8_t* s_region = nullptr;
     uint64_t* s_fit = nullptr;
@@ -1253,7 +1253,7 @@ int sparc_destroy(void* ctx) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->vis, c->dirs, c->pos, c->aux, c->step, c->pid, c->t_open, c->t_info, c->t_root, c->t_trie, c->t_trie1, c->t_init, c->t_row1,
                     c->t_trie8, c->t_trow, c->t_mrow, c->t_mroww, c->t_boardw, c->err, c->s_act, c->s_flags, c->s_mask, c->s_rew, c->s_pidx, c->r_planes, c->r_inst_range,
-                    c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off, c->r_memo, c->s_bits, c->s_region, c->s_fit, c->r_fit_off, c->r_fit_tab};
+                    c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off, c->r_memo, c->s_bits, c->s_region, c->s_fit, c->r_reg_off, c->r_reg_tab};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->own) (void)hipStreamDestroy(c->own);
@@ -1801,7 +1801,7 @@ int sparc_rollout_rules_device(void* ctx, int32_t T, const uint8_t* d_act, uint6
     if (!c->rules) return fail(c, SPARC_E_STATE, "sparc_load_rules has not been called");
     if (!d_rule_bits) return fail(c, SPARC_E_INVALID, "null rule_bits");
     const RuleTrace rtr{RulesTab{c->r_planes, c->r_inst_range, c->r_inst, c->r_shape_range, c->r_shape_area,
-                                 c->r_shape_off, c->num_puzzles, c->r_area ? 1u : 0u, c->r_fit_off, c->r_fit_tab},
+                                 c->r_shape_off, c->num_puzzles, c->r_area ? 1u : 0u, c->r_reg_off, c->r_reg_tab},
                         d_rule_bits, c->r_memo};
     return rollout_impl(c, T, d_act, seed, t0, d_rew, d_flags, d_stats, nullptr, &rtr);
 }
@@ -1911,12 +1911,12 @@ int sparc_load_rules(void* ctx, const sparc_rules_table* t) {
         }
     }
     void* old[] = {c->r_planes, c->r_inst_range, c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off,
-                   c->r_fit_off, c->r_fit_tab};
+                   c->r_reg_off, c->r_reg_tab};
     for (void* b : old)
         if (b) HIPCHK(c, hipFree(b));
     c->r_planes = nullptr; c->r_inst_range = nullptr; c->r_inst = nullptr;
     c->r_shape_range = nullptr; c->r_shape_area = nullptr; c->r_shape_off = nullptr;
-    c->r_fit_off = nullptr; c->r_fit_tab = nullptr;
+    c->r_reg_off = nullptr; c->r_reg_tab = nullptr;
     c->rules = false;
     // the device copy: the caller's SPARC_RULE_PLANES planes per puzzle, RP_INST rewritten from the
     // instance list, then the bit-sliced net area of each cell (kAreaPlanes planes, sparc_rules.hpp)
@@ -1962,36 +1962,39 @@ int sparc_load_rules(void* ctx, const sparc_rules_table* t) {
     // the memo's entries name puzzles of the old table: start empty (a zero key matches no region)
     if (!c->r_memo) HIPCHK(c, hipMalloc(&c->r_memo, sizeof(FitMemo<kMemo>) * (size_t)c->n));
     HIPCHK(c, hipMemset(c->r_memo, 0, sizeof(FitMemo<kMemo>) * (size_t)c->n));
-    // the exact-fit answer of every region cell mask of each puzzle with at most kFitTabCells
-    // cells, computed once here by the audit's own search (k_fit_table): the audit then looks
-    // answers up instead of searching (the memo serves the larger puzzles)
-    std::vector<uint32_t> fit_off(P, kNoFitTab);
+    // the per-region check code (squares, stars, poly/ylop area + exact fit) of every region cell
+    // mask of each puzzle with at most kRegTabCells cells, computed once here by the audit's own
+    // region_code (k_region_table): the audit then looks codes up per region instead of running
+    // the checks (the memo serves the larger puzzles).  At most 128 MB of table.
+    std::vector<uint32_t> reg_off(P, kNoRegTab);
     std::vector<uint2> items;
     size_t entries = 0;
+    constexpr size_t kMaxRegEntries = (size_t)1 << 28;
     for (size_t q = 0; q < P; ++q) {
         const uint32_t X = info[q].x & 0xFFu, Y = (info[q].x >> 8) & 0xFFu;
         const uint32_t cells = ((X - 1) / 2) * ((Y - 1) / 2);
-        if (cells > kFitTabCells || (t->inst_range[q] >> 16) == 0) continue;
-        const uint32_t words = cells <= 4 ? 1u : 1u << (cells - 4);
-        fit_off[q] = (uint32_t)entries;
+        if (cells > kRegTabCells) continue;
+        const uint32_t words = cells <= 3 ? 1u : 1u << (cells - 3);
+        if (entries + 8u * words > kMaxRegEntries) break;
+        reg_off[q] = (uint32_t)entries;
         for (uint32_t g = 0; g < words; ++g) items.push_back(make_uint2((uint32_t)q, g));
-        entries += 16u * words;
+        entries += 8u * words;
     }
     if (!items.empty()) {
-        const size_t words = entries / 16;
+        const size_t words = entries / 8;
         uint2* d_items = nullptr;
-        HIPCHK(c, hipMalloc(&c->r_fit_off, sizeof(uint32_t) * P));
-        HIPCHK(c, hipMalloc(&c->r_fit_tab, sizeof(uint32_t) * words));
+        HIPCHK(c, hipMalloc(&c->r_reg_off, sizeof(uint32_t) * P));
+        HIPCHK(c, hipMalloc(&c->r_reg_tab, sizeof(uint32_t) * words));
         HIPCHK(c, hipMalloc(&d_items, sizeof(uint2) * items.size()));
-        HIPCHK(c, hipMemcpy(c->r_fit_off, fit_off.data(), sizeof(uint32_t) * P, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(c->r_reg_off, reg_off.data(), sizeof(uint32_t) * P, hipMemcpyHostToDevice));
         HIPCHK(c, hipMemcpy(d_items, items.data(), sizeof(uint2) * items.size(), hipMemcpyHostToDevice));
         const Params p = make_params(c);
         const RulesTab rt{c->r_planes, c->r_inst_range, c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off,
-                          c->num_puzzles, c->r_area ? 1u : 0u, c->r_fit_off, nullptr};
+                          c->num_puzzles, c->r_area ? 1u : 0u, c->r_reg_off, nullptr};
         const dim3 g((unsigned)((items.size() + kBlock - 1) / kBlock));
-        if (W == 1) k_fit_table<1><<<g, kBlock, 0, c->stream>>>(p, rt, d_items, (uint32_t)items.size(), c->r_fit_tab);
-        else if (W == 2) k_fit_table<2><<<g, kBlock, 0, c->stream>>>(p, rt, d_items, (uint32_t)items.size(), c->r_fit_tab);
-        else k_fit_table<4><<<g, kBlock, 0, c->stream>>>(p, rt, d_items, (uint32_t)items.size(), c->r_fit_tab);
+        if (W == 1) k_region_table<1><<<g, kBlock, 0, c->stream>>>(p, rt, d_items, (uint32_t)items.size(), c->r_reg_tab);
+        else if (W == 2) k_region_table<2><<<g, kBlock, 0, c->stream>>>(p, rt, d_items, (uint32_t)items.size(), c->r_reg_tab);
+        else k_region_table<4><<<g, kBlock, 0, c->stream>>>(p, rt, d_items, (uint32_t)items.size(), c->r_reg_tab);
         rc = launch_check(c);
         HIPCHK(c, hipStreamSynchronize(c->stream));
         HIPCHK(c, hipFree(d_items));
@@ -2009,7 +2012,7 @@ int sparc_rules_device(void* ctx, uint16_t* d_bits, uint8_t* d_region, uint64_t*
     if (!c->rules) return fail(c, SPARC_E_STATE, "sparc_load_rules has not been called");
     const Params p = make_params(c);
     const RulesTab rt{c->r_planes, c->r_inst_range, c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off,
-                      c->num_puzzles, c->r_area ? 1u : 0u, c->r_fit_off, c->r_fit_tab};
+                      c->num_puzzles, c->r_area ? 1u : 0u, c->r_reg_off, c->r_reg_tab};
     const dim3 g = grid_for(c->n);
     if (c->W == 1) k_rules<1><<<g, kBlock, 0, c->stream>>>(p, rt, d_bits, d_region, d_fit, c->r_memo);
     else if (c->W == 2) k_rules<2><<<g, kBlock, 0, c->stream>>>(p, rt, d_bits, d_region, d_fit, c->r_memo);

@@ -62,15 +62,15 @@ struct RulesTab {
     const int8_t* __restrict__ shape_off;     // [offsets][2] (dcx, dcy) in cell units
     uint32_t num_puzzles;
     uint32_t area;   // 1: the RP_AREA planes hold every cell's net area (else the list is walked)
-    // exact-fit answers of every region cell mask of the puzzles with at most kFitTabCells cells
-    // (sparc_load_rules runs exact_fit over all of them once): fit_off[q] = the puzzle's first
-    // entry (a multiple of 16) or kNoFitTab; entries of 2 bits, 16 per word of fit_tab:
-    // 0 no fit, 1 fits, 2 search exhausted.  May be null (no table).
-    const uint32_t* __restrict__ fit_off;
-    const uint32_t* __restrict__ fit_tab;
+    // the per-region check codes (region_code) of every region cell mask of each puzzle with at
+    // most kRegTabCells cells, computed once by sparc_load_rules: reg_off[q] = the puzzle's first
+    // entry (a multiple of 8) or kNoRegTab; entries of 4 bits, 8 per word of reg_tab.  May be
+    // null (no table).
+    const uint32_t* __restrict__ reg_off;
+    const uint32_t* __restrict__ reg_tab;
 };
-constexpr uint32_t kNoFitTab = 0xFFFFFFFFu;
-constexpr uint32_t kFitTabCells = 12;
+constexpr uint32_t kNoRegTab = 0xFFFFFFFFu;
+constexpr uint32_t kRegTabCells = 12;
 
 template <int W>
 struct BB {
@@ -164,13 +164,31 @@ __device__ __forceinline__ void fit_shape(const RulesTab& rt, uint32_t sh, uint3
         for (int ay = -mdy0; ay + mdy1 < (int)CY; ++ay) va |= 1ull << (ax * (int)CY + ay);
 }
 
-// the region's cells on the exact fit's cell grid (bit cx * CY + cy)
+// the region's cells on the exact fit's cell grid (bit cx * CY + cy): per cell row, the 32 board
+// bits from the row's first cell centre, the cell centres (every other bit, CY <= 7) kept and
+// compressed with three shift-or-mask steps
+template <int W>
+__device__ __forceinline__ uint32_t bits32_at(const BB<W>& b, uint32_t pos) {
+    const uint32_t k = pos >> 6, r = pos & 63u;
+    uint64_t lo = 0, hi = 0;
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+        lo = (uint32_t)j == k ? b.w[j] : lo;
+        hi = (uint32_t)j == k + 1 ? b.w[j] : hi;
+    }
+    return (uint32_t)((lo >> r) | (r ? hi << (64 - r) : 0ull));
+}
 template <int W>
 __device__ __forceinline__ uint64_t cell_mask(const FitIn& in, const BB<W>& Rc, uint32_t pitch) {
+    const uint32_t alt = 0x1555u & ((1u << (2 * in.CY - 1)) - 1u);   // cell centres of one row
     uint64_t rm = 0;
-    for (uint32_t cx = 0; cx < in.CX; ++cx)
-        for (uint32_t cy = 0; cy < in.CY; ++cy)
-            if (Rc.test((2 * cx + 1) * pitch + 2 * cy + 1)) rm |= 1ull << (cx * in.CY + cy);
+    for (uint32_t cx = 0; cx < in.CX; ++cx) {
+        uint32_t v = bits32_at<W>(Rc, (2 * cx + 1) * pitch + 1) & alt;
+        v = (v | (v >> 1)) & 0x3333u;
+        v = (v | (v >> 2)) & 0x0F0Fu;
+        v = (v | (v >> 4)) & 0x00FFu;
+        rm |= (uint64_t)v << (cx * in.CY);
+    }
     return rm;
 }
 
@@ -336,27 +354,74 @@ __device__ __forceinline__ bool region_net_area(const RulesTab& rt, const FitIn&
     return has;
 }
 
-// One entry word of the fit table: the exact-fit answers of region cell masks 16·g .. 16·g + 15
-// of puzzle q (masks whose area check fails, or with no instance, are never looked up: 0).
+// ---------------------------------------------------------------- per-region checks
+// The per-region rules of region cells Rc (rm: its cell mask), as a 4-bit code: bit 0 squares
+// ok (533-551: at most one non-zero colour), bit 1 stars ok (553-619: no colourless star, and
+// for each star colour c exactly 2 symbol occurrences of colour c), bits 2-3 the poly / ylop
+// check (648-838): 0 no instance in the region, 1 passed (area and exact fit), 2 failed, 3 the
+// exact-fit search was exhausted.  pl: the puzzle's SPARC_RULE_PLANES planes.
+enum : uint32_t { kRcSq = 1u, kRcStar = 2u, kRcPolyShift = 2u };
+template <int W, class Memo>
+__device__ uint32_t region_code(const RulesTab& rt, const FitIn& fin, uint32_t q, const BB<W>& Rc, uint64_t rm,
+                                const BB<W>* pl, Memo* memo) {
+    uint32_t code = kRcSq | kRcStar;
+    const BB<W> sq = Rc & pl[RP_SQUARE];
+    if (sq.any()) {
+        int ncol = 0;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) ncol += (sq & pl[RP_COL1 + c]).any();
+        if (ncol > 1) code &= ~kRcSq;
+    }
+    const BB<W> st = Rc & pl[RP_STAR];
+    if (st.any()) {
+        bool ok = !st.andnot(pl[RP_COLORED]).any();
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const BB<W> col = Rc & pl[RP_COL1 + c];
+            if (!(st & col).any()) continue;
+            const int tot = (col & pl[RP_M0]).popc() + 2 * (col & pl[RP_M1]).popc() + 4 * (col & pl[RP_M2]).popc();
+            ok &= tot == 2;
+        }
+        if (!ok) code &= ~kRcStar;
+    }
+    int net;
+    if (region_net_area<W>(rt, fin, q, Rc, pl[RP_INST], net)) {
+        uint32_t poly = 2;
+        if (Rc.popc() == net) {
+            int r = -1;
+            if constexpr (!std::is_same<Memo, NoMemo>::value) r = memo->find(q, rm);
+            if (r < 0) {
+                r = exact_fit<W>(fin, Rc, rm);
+                if constexpr (!std::is_same<Memo, NoMemo>::value)
+                    if (r >= 0) memo->put(q, rm, r);
+            }
+            poly = r < 0 ? 3u : (r ? 1u : 2u);
+        }
+        code |= poly << kRcPolyShift;
+    }
+    return code;
+}
+
+// One word of the region-code table: the codes of region cell masks 8·g .. 8·g + 7 of puzzle q
+// (4 bits each; masks that are no region of any state are never looked up).
 template <int W>
-__device__ uint32_t fit_table_word(const Params& p, const RulesTab& rt, uint32_t q, uint32_t g) {
+__device__ uint32_t region_table_word(const Params& p, const RulesTab& rt, uint32_t q, uint32_t g) {
     const uint4 inf = p.tab.info[q];
     const uint32_t X = inf.x & 0xFFu, Y = (inf.x >> 8) & 0xFFu;
     const uint32_t ir = rt.inst_range[q];
     const FitIn fin{&rt, ir & 0xFFFFu, ir >> 16, (X - 1) / 2, (Y - 1) / 2};
     const uint32_t cells = fin.CX * fin.CY;
-    const BB<W> inst_plane = BB<W>::load(rt.planes + ((size_t)q * RP_COUNT + RP_INST) * W);
+    BB<W> pl[RP_ABI];
+    const uint64_t* gp = rt.planes + (size_t)q * RP_COUNT * W;
+    for (int k = 0; k < (int)RP_ABI; ++k) pl[k] = BB<W>::load(gp + k * W);
     uint32_t word = 0;
-    for (uint32_t j = 0; j < 16; ++j) {
-        const uint32_t m = 16u * g + j;
+    for (uint32_t j = 0; j < 8; ++j) {
+        const uint32_t m = 8u * g + j;
         if (m == 0 || m >= (1u << cells)) continue;
         BB<W> Rc = BB<W>::zero();
         for (uint32_t b = 0; b < cells; ++b)
             if ((m >> b) & 1u) Rc.set((2 * (b / fin.CY) + 1) * p.pitch + 2 * (b % fin.CY) + 1);
-        int net;
-        if (!region_net_area<W>(rt, fin, q, Rc, inst_plane, net) || Rc.popc() != net) continue;
-        const int r = exact_fit<W>(fin, Rc, (uint64_t)m);
-        word |= (r < 0 ? 2u : (uint32_t)r) << (2 * j);
+        word |= region_code<W, NoMemo>(rt, fin, q, Rc, (uint64_t)m, pl, nullptr) << (4 * j);
     }
     return word;
 }
@@ -369,16 +434,24 @@ struct RuleOut {
 };
 
 // vis: path points; x, y: agent; q: puzzle.  region_out (may be null): region id per bit.
-// memo (FitMemo, or NoMemo): exact-fit answers carried between calls of one lane.
+// memo (FitMemo, or NoMemo): exact-fit answers carried between calls of one lane (puzzles
+// without a region-code table).
 template <int W, class Memo = NoMemo>
 __device__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const BB<W>& vis, uint32_t x, uint32_t y,
                             uint32_t q, uint8_t* region_out, Memo* memo = nullptr) {
-    // every plane of the puzzle in registers up front: one round of loads, none in the loops
+    const uint32_t fo = rt.reg_off ? rt.reg_off[q] : kNoRegTab;
+    const uint64_t* g = rt.planes + (size_t)q * RP_COUNT * W;
+    // the planes the regions and the path rules need, in registers up front (one round of loads);
+    // the symbol planes only for a puzzle without a region-code table
     BB<W> pl[RP_ABI];
-    {
-        const uint64_t* g = rt.planes + (size_t)q * RP_COUNT * W;
+    constexpr uint32_t kBase[] = {RP_CELLS, RP_LATTICE, RP_GAPS, RP_DOTS, RP_TRI, RP_TRI0, RP_TRI1, RP_TRI2,
+                                  RP_NOTFIRST, RP_NOTLAST};
 #pragma unroll
-        for (int k = 0; k < (int)RP_ABI; ++k) pl[k] = BB<W>::load(g + k * W);
+    for (uint32_t k : kBase) pl[k] = BB<W>::load(g + k * W);
+    if (fo == kNoRegTab) {
+#pragma unroll
+        for (uint32_t k = RP_STAR; k <= RP_M2; ++k) pl[k] = BB<W>::load(g + k * W);
+        pl[RP_INST] = BB<W>::load(g + RP_INST * W);
     }
     const uint4 inf = p.tab.info[q];
     const uint32_t X = inf.x & 0xFFu, Y = (inf.x >> 8) & 0xFFu;
@@ -391,10 +464,20 @@ __device__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const BB<W>& vi
     const BB<W> allowed = lattice.andnot(gaps | vis) | cells;
     const uint32_t ir = rt.inst_range[q];
     const FitIn fin{&rt, ir & 0xFFFFu, ir >> 16, (X - 1) / 2, (Y - 1) / 2};
-    const uint32_t fo = rt.fit_off ? rt.fit_off[q] : kNoFitTab;
 
     bool sq_ok = true, star_ok = true, poly_ok = true, exhausted = false;
     uint64_t fit_ok = 0;
+    auto take = [&](uint32_t code, uint32_t r) {
+        sq_ok &= (code & kRcSq) != 0;
+        star_ok &= (code & kRcStar) != 0;
+        const uint32_t poly = code >> kRcPolyShift;
+        exhausted |= poly == 3u;
+        poly_ok &= poly < 2u;
+        if (poly == 1u) fit_ok |= 1ull << (r & 63);
+    };
+    // a table lookup is consumed one region later, so its L2 latency overlaps the next flood fill
+    uint32_t tw = 0, tsh = 0, trid = 0;
+    bool tpend = false;
     BB<W> remaining = cells;
     uint32_t rid = 0;
     while (remaining.any()) {
@@ -416,54 +499,21 @@ __device__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const BB<W>& vi
                 t.w[b >> 6] &= t.w[b >> 6] - 1;
             }
         }
-        // squares: at most one non-zero colour (533-551)
-        const BB<W> sq = Rc & pl[RP_SQUARE];
-        if (sq.any()) {
-            int ncol = 0;
-#pragma unroll
-            for (int c = 0; c < 8; ++c) ncol += (sq & pl[RP_COL1 + c]).any();
-            sq_ok &= ncol <= 1;
-        }
-        // stars (553-619)
-        const BB<W> st = Rc & pl[RP_STAR];
-        if (st.any()) {
-            star_ok &= !st.andnot(pl[RP_COLORED]).any();
-            const BB<W> m0 = pl[RP_M0], m1 = pl[RP_M1], m2 = pl[RP_M2];
-#pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                const BB<W> col = Rc & pl[RP_COL1 + c];
-                if (!(st & col).any()) continue;
-                const int tot = (col & m0).popc() + 2 * (col & m1).popc() + 4 * (col & m2).popc();
-                star_ok &= tot == 2;
-            }
-        }
-        // poly / ylop (648-709)
-        int net;
-        if (region_net_area<W>(rt, fin, q, Rc, pl[RP_INST], net)) {
-            bool ok = Rc.popc() == net;
-            if (ok) {
-                const uint64_t rm = cell_mask<W>(fin, Rc, P);
-                int r = -1;
-                if (fo != kNoFitTab) {                         // the precomputed answer
-                    const uint32_t m = (uint32_t)rm;
-                    const uint32_t a = (rt.fit_tab[(fo + m) >> 4] >> ((m & 15u) * 2u)) & 3u;
-                    r = a == 2u ? -1 : (int)a;
-                } else {
-                    if constexpr (!std::is_same<Memo, NoMemo>::value) r = memo->find(q, rm);
-                    if (r < 0) {
-                        r = exact_fit<W>(fin, Rc, rm);
-                        if constexpr (!std::is_same<Memo, NoMemo>::value)
-                            if (r >= 0) memo->put(q, rm, r);
-                    }
-                }
-                exhausted |= r < 0;
-                ok = r > 0;
-            }
-            if (ok) fit_ok |= 1ull << (rid & 63);
-            poly_ok &= ok;
+        const uint64_t rm = cell_mask<W>(fin, Rc, P);
+        if (tpend) take((tw >> tsh) & 15u, trid);
+        tpend = false;
+        if (fo != kNoRegTab) {                                   // the precomputed code
+            const uint32_t m = (uint32_t)rm;
+            tw = rt.reg_tab[(fo + m) >> 3];
+            tsh = (m & 7u) * 4u;
+            trid = rid;
+            tpend = true;
+        } else {
+            take(region_code<W, Memo>(rt, fin, q, Rc, rm, pl, memo), rid);
         }
         ++rid;
     }
+    if (tpend) take((tw >> tsh) & 15u, trid);
     // triangles: bit-sliced count of path neighbours (x±1: ±P, y±1: ±1)
     const BB<W> a = vis.shr(P), b = vis.shl(P), c = vis.shr(1), d = vis.shl(1);
     const BB<W> s1 = a ^ b, c1 = a & b, s2 = c ^ d, c2 = c & d;
