@@ -359,6 +359,8 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
     // exact-fit answers of this lane's recent regions (the path moves one point per step),
     // carried between launches and audit calls in HBM
     FitMemo<kMemo> memo;
+    PuzzleRules<W> pr;   // W = 1 rule rollouts: the env's puzzle rule data (pr.q = its puzzle)
+    pr.q = 0xFFFFFFFFu;
     if constexpr (RULES)
         if (rtr.memo && i < p.n) memo = rtr.memo[i];
     auto audit_step = [&](int32_t t) {               // rule bits of the state after step t
@@ -370,7 +372,14 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
 #pragma unroll
             for (int k = 0; k < W; ++k) vb.w[k] = v[k];
             const uint32_t xy = e.agent_xy(p);
-            const RuleOut<W> ro = audit<W>(p, rtr.rt, vb, xy & 0xFFu, (xy >> 8) & 0xFFu, e.pid, nullptr, &memo);
+            RuleOut<W> ro;
+            if constexpr (W == 1) {   // the puzzle's rule data stays in registers until the env's puzzle changes
+                if (e.pid != pr.q) pr = puzzle_rules<W>(p, rtr.rt, e.pid);
+                ro = audit<W>(p, rtr.rt, pr, vb, xy & 0xFFu, (xy >> 8) & 0xFFu, nullptr, &memo);
+            } else {
+                ro = audit<W>(p, rtr.rt, puzzle_rules<W>(p, rtr.rt, e.pid), vb, xy & 0xFFu, (xy >> 8) & 0xFFu, nullptr,
+                              &memo);
+            }
             rtr.bits[(size_t)t * n + i] = (uint16_t)ro.bits;
         }
     };
@@ -1025,7 +1034,7 @@ __global__ void __launch_bounds__(kBlock) k_rules(Params p, RulesTab rt, uint16_
     // the env's exact-fit memo: the reference audits every step() (SPaRC_Gym.py:1227), and
     // consecutive states share most regions
     FitMemo<kMemo> memo = memos[i];
-    const RuleOut<W> r = audit<W>(p, rt, vis, ps & 0xFFu, (ps >> 8) & 0xFFu, q, ro, &memo);
+    const RuleOut<W> r = audit<W>(p, rt, puzzle_rules<W>(p, rt, q), vis, ps & 0xFFu, (ps >> 8) & 0xFFu, ro, &memo);
     memos[i] = memo;
     if (bits) bits[i] = (uint16_t)r.bits;
     if (fit) fit[i] = r.fit_ok;

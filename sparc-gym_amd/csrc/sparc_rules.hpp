@@ -433,37 +433,57 @@ struct RuleOut {
     uint64_t fit_ok;   // bit r: region r held instances and passed the area check and the fit
 };
 
-// vis: path points; x, y: agent; q: puzzle.  region_out (may be null): region id per bit.
-// memo (FitMemo, or NoMemo): exact-fit answers carried between calls of one lane (puzzles
-// without a region-code table).
-template <int W, class Memo = NoMemo>
-__device__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const BB<W>& vis, uint32_t x, uint32_t y,
-                            uint32_t q, uint8_t* region_out, Memo* memo = nullptr) {
-    const uint32_t fo = rt.reg_off ? rt.reg_off[q] : kNoRegTab;
+// What the audit reads of puzzle q besides the state: the planes the regions and the path rules
+// need, the target, the cell grid and the region-code table offset (a rule rollout keeps it in
+// registers while the env stays on its puzzle).
+template <int W>
+struct PuzzleRules {
+    BB<W> pl[10];   // kBasePlanes order
+    uint32_t q, fo, tx, ty;
+    FitIn fin;
+};
+constexpr uint32_t kBasePlanes[10] = {RP_CELLS, RP_LATTICE, RP_GAPS, RP_DOTS, RP_TRI, RP_TRI0, RP_TRI1, RP_TRI2,
+                                      RP_NOTFIRST, RP_NOTLAST};
+enum : uint32_t { kB_CELLS = 0, kB_LATTICE, kB_GAPS, kB_DOTS, kB_TRI, kB_TRI0, kB_TRI1, kB_TRI2, kB_NOTFIRST, kB_NOTLAST };
+template <int W>
+__device__ __forceinline__ PuzzleRules<W> puzzle_rules(const Params& p, const RulesTab& rt, uint32_t q) {
+    PuzzleRules<W> r;
     const uint64_t* g = rt.planes + (size_t)q * RP_COUNT * W;
-    // the planes the regions and the path rules need, in registers up front (one round of loads);
+#pragma unroll
+    for (int k = 0; k < 10; ++k) r.pl[k] = BB<W>::load(g + kBasePlanes[k] * W);
+    const uint4 inf = p.tab.info[q];
+    const uint32_t X = inf.x & 0xFFu, Y = (inf.x >> 8) & 0xFFu;
+    const uint32_t ir = rt.inst_range[q];
+    r.q = q;
+    r.fo = rt.reg_off ? rt.reg_off[q] : kNoRegTab;
+    r.tx = inf.y & 0xFFu;
+    r.ty = (inf.y >> 8) & 0xFFu;
+    r.fin = FitIn{&rt, ir & 0xFFFFu, ir >> 16, (X - 1) / 2, (Y - 1) / 2};
+    return r;
+}
+
+// vis: path points; x, y: agent; pr: the env's puzzle (puzzle_rules).  region_out (may be
+// null): region id per bit.  memo (FitMemo, or NoMemo): exact-fit answers carried between calls
+// of one lane (puzzles without a region-code table).
+template <int W, class Memo = NoMemo>
+__device__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const PuzzleRules<W>& pr, const BB<W>& vis,
+                            uint32_t x, uint32_t y, uint8_t* region_out, Memo* memo = nullptr) {
+    const uint32_t q = pr.q, fo = pr.fo;
+    const FitIn& fin = pr.fin;
     // the symbol planes only for a puzzle without a region-code table
     BB<W> pl[RP_ABI];
-    constexpr uint32_t kBase[] = {RP_CELLS, RP_LATTICE, RP_GAPS, RP_DOTS, RP_TRI, RP_TRI0, RP_TRI1, RP_TRI2,
-                                  RP_NOTFIRST, RP_NOTLAST};
-#pragma unroll
-    for (uint32_t k : kBase) pl[k] = BB<W>::load(g + k * W);
     if (fo == kNoRegTab) {
+        const uint64_t* g = rt.planes + (size_t)q * RP_COUNT * W;
 #pragma unroll
         for (uint32_t k = RP_STAR; k <= RP_M2; ++k) pl[k] = BB<W>::load(g + k * W);
         pl[RP_INST] = BB<W>::load(g + RP_INST * W);
     }
-    const uint4 inf = p.tab.info[q];
-    const uint32_t X = inf.x & 0xFFu, Y = (inf.x >> 8) & 0xFFu;
-    const uint32_t tx = inf.y & 0xFFu, ty = (inf.y >> 8) & 0xFFu;
+    const uint32_t tx = pr.tx, ty = pr.ty;
     const uint32_t P = p.pitch;
-    const BB<W> cells = pl[RP_CELLS];
-    const BB<W> lattice = pl[RP_LATTICE];
-    const BB<W> gaps = pl[RP_GAPS];
-    const BB<W> nfirst = pl[RP_NOTFIRST], nlast = pl[RP_NOTLAST];
-    const BB<W> allowed = lattice.andnot(gaps | vis) | cells;
-    const uint32_t ir = rt.inst_range[q];
-    const FitIn fin{&rt, ir & 0xFFFFu, ir >> 16, (X - 1) / 2, (Y - 1) / 2};
+    const BB<W> cells = pr.pl[kB_CELLS];
+    const BB<W> gaps = pr.pl[kB_GAPS];
+    const BB<W> nfirst = pr.pl[kB_NOTFIRST], nlast = pr.pl[kB_NOTLAST];
+    const BB<W> allowed = pr.pl[kB_LATTICE].andnot(gaps | vis) | cells;
 
     bool sq_ok = true, star_ok = true, poly_ok = true, exhausted = false;
     uint64_t fit_ok = 0;
@@ -518,11 +538,11 @@ __device__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const BB<W>& vi
     const BB<W> a = vis.shr(P), b = vis.shl(P), c = vis.shr(1), d = vis.shl(1);
     const BB<W> s1 = a ^ b, c1 = a & b, s2 = c ^ d, c2 = c & d;
     const BB<W> n0 = s1 ^ s2, k0 = s1 & s2, n1 = c1 ^ c2 ^ k0, n2 = c1 & c2;
-    const BB<W> bad = pl[RP_TRI] & ((n0 ^ pl[RP_TRI0]) | (n1 ^ pl[RP_TRI1]) | (n2 ^ pl[RP_TRI2]));
+    const BB<W> bad = pr.pl[kB_TRI] & ((n0 ^ pr.pl[kB_TRI0]) | (n1 ^ pr.pl[kB_TRI1]) | (n2 ^ pr.pl[kB_TRI2]));
     const bool tri_ok = !bad.any();
     const bool reached = x == tx && y == ty;
     const bool gap_ok = !(gaps & vis).any();
-    const bool dot_ok = !pl[RP_DOTS].andnot(vis).any();
+    const bool dot_ok = !pr.pl[kB_DOTS].andnot(vis).any();
     uint32_t bits = (uint32_t)reached | 2u | ((uint32_t)gap_ok << 2) | ((uint32_t)dot_ok << 3) |
                     ((uint32_t)sq_ok << 4) | ((uint32_t)star_ok << 5) | ((uint32_t)tri_ok << 6) |
                     ((uint32_t)poly_ok << 7);
