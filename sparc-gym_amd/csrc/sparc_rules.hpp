@@ -192,6 +192,17 @@ __device__ __forceinline__ uint64_t cell_mask(const FitIn& in, const BB<W>& Rc, 
     return rm;
 }
 
+// cell_mask of a one-word board of pitch 8 (every pool up to 7 x 7): lattice row x is byte x,
+// so the cell rows (bytes 1, 3, 5) come together in one v_perm_b32 and their centres (bits 1, 3,
+// 5 of each byte, CY <= 3) compress in all three bytes at once
+__device__ __forceinline__ uint64_t cell_mask_p8(const FitIn& in, uint64_t rc) {
+    uint32_t w = __builtin_amdgcn_perm((uint32_t)(rc >> 32), (uint32_t)rc, 0x0C050301u);
+    w = (w >> 1) & 0x151515u;
+    w = (w | (w >> 1)) & 0x131313u;
+    w = (w | (w >> 2)) & 0x070707u;
+    return (w & 7u) | (((w >> 8) & 7u) << in.CY) | (((w >> 16) & 7u) << (2 * in.CY));
+}
+
 // _polyfit_region_exact with the area check passed (so net = area > 0 and the grid starts at
 // -1 on the region's cells), as a depth-first search over the same choices (existence only:
 // identical ylops take non-decreasing anchors, polys are tried by distinct shape).  Returns 1 (fits),
@@ -504,7 +515,11 @@ __device__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const PuzzleRul
         BB<W> R = BB<W>::zero();
         R.set(remaining.lowest());
         while (true) {                                           // flood fill (BFS 431-452)
-            BB<W> N = R | (R.shl(1) & nfirst) | (R.shr(1) & nlast) | R.shl(P) | R.shr(P);
+            BB<W> N;
+            if constexpr (W == 1)   // the padded one-word geometry: a y step off the lattice lands on a blocked bit
+                N = R | R.shl(1) | R.shr(1) | R.shl(P) | R.shr(P);
+            else
+                N = R | (R.shl(1) & nfirst) | (R.shr(1) & nlast) | R.shl(P) | R.shr(P);
             N = N & allowed;
             if (N == R) break;
             R = N;
@@ -519,7 +534,11 @@ __device__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const PuzzleRul
                 t.w[b >> 6] &= t.w[b >> 6] - 1;
             }
         }
-        const uint64_t rm = cell_mask<W>(fin, Rc, P);
+        uint64_t rm;
+        if constexpr (W == 1)
+            rm = P == 8u ? cell_mask_p8(fin, Rc.w[0]) : cell_mask<W>(fin, Rc, P);
+        else
+            rm = cell_mask<W>(fin, Rc, P);
         if (tpend) take((tw >> tsh) & 15u, trid);
         tpend = false;
         if (fo != kNoRegTab) {                                   // the precomputed code

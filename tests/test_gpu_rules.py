@@ -121,8 +121,8 @@ def test_rules_at_scale_vs_oracle(on_gpu, sizes, full, n, max_shaped):
     assert checked == 1200
 
 
-@pytest.mark.parametrize("sizes,max_shaped", [(((3, 3),), None), (((2, 2), (3, 3), (4, 4), (5, 5)), None),
-                                              (((7, 7), (6, 6)), 4)])
+@pytest.mark.parametrize("sizes,max_shaped", [(((3, 3),), None), (((2, 3), (3, 2), (2, 2), (1, 3)), None),
+                                              (((2, 2), (3, 3), (4, 4), (5, 5)), None), (((7, 7), (6, 6)), 4)])
 def test_rollout_rule_bits_every_step(on_gpu, sizes, max_shaped):
     """rollout(rules=True): the audit after every step inside the rollout launch (the reference
     audits every step(), SPaRC_Gym.py:1227) equals step()-by-step() rule_audit() bits, and the
