@@ -40,6 +40,9 @@ constexpr int kWaves = kBlock / 64;
 // per wave
 template <int W, int EPW>
 __host__ __device__ constexpr size_t tiles_lds_bytes() { return (size_t)kWaves * 3 * EPW * kTile; }
+// per-wave LDS tile of the rule bits of a rule rollout ([16 steps][EPW envs] uint16)
+template <int EPW>
+__host__ __device__ constexpr size_t bits_lds_bytes() { return (size_t)kWaves * 2 * EPW * kTile; }
 constexpr size_t kMaxDynLds = 160 * 1024;   // one workgroup may own all 160 KiB (gfx950)
 
 // LDS bytes of the staged puzzle rows: (W = 1) compact row + reset board, or (W > 1) info +
@@ -296,7 +299,9 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
     uint8_t* tf = tr + EPW * kTile;
     constexpr size_t kStackOff = tiles_lds_bytes<W, EPW>();
     constexpr size_t kObsOff = kStackOff + stack_lds_bytes<W, TB, EPW>();
-    constexpr size_t kTableOff = kObsOff + (OBS ? obs_lds_bytes<W>() : 0);
+    constexpr size_t kBitsOff = kObsOff + (OBS ? obs_lds_bytes<W>() : 0);
+    constexpr size_t kTableOff = kBitsOff + (RULES ? bits_lds_bytes<EPW>() : 0);
+    uint16_t* tbits = reinterpret_cast<uint16_t*>(smem + kBitsOff) + wv * (EPW * kTile);
     PuzzleSrc<W> src{p.tab.info, p.tab.root, p.tab.open, p.tab.init, p.tab.row1};
     ObsWave<W>* ow = reinterpret_cast<ObsWave<W>*>(smem + kObsOff) + wv;
     const uint16_t* lut = reinterpret_cast<const uint16_t*>(smem + kObsOff + kWaves * sizeof(ObsWave<W>));
@@ -363,7 +368,7 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
     pr.q = 0xFFFFFFFFu;
     if constexpr (RULES)
         if (rtr.memo && i < p.n) memo = rtr.memo[i];
-    auto audit_step = [&](int32_t t) {               // rule bits of the state after step t
+    auto audit_step = [&](int32_t t, uint16_t* slot) {   // rule bits of the state after step t -> slot
         if constexpr (RULES) {
             uint64_t v[W];
             uint32_t ab;
@@ -380,7 +385,7 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
                 ro = audit<W>(p, rtr.rt, puzzle_rules<W>(p, rtr.rt, e.pid), vb, xy & 0xFFu, (xy >> 8) & 0xFFu, nullptr,
                               &memo);
             }
-            rtr.bits[(size_t)t * n + i] = (uint16_t)ro.bits;
+            *slot = (uint16_t)ro.bits;
         }
     };
     u32x4 anext = {0u, 0u, 0u, 0u};
@@ -409,7 +414,7 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
                     uint32_t f;
                     const int code = e.advance(p, src, av[j], f);
                     obs(tb + k);
-                    audit_step(tb + k);
+                    audit_step(tb + k, tbits + k * EPW + lane);
                     tr[k * EPW + lane] = (uint8_t)code;
                     tf[k * EPW + lane] = (uint8_t)f;
                     if constexpr (W == 1) {   // per-step flags the W = 1 step already has
@@ -429,6 +434,15 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
             const size_t o = (size_t)(tb + r) * n + wave_base + c;
             if (rew) nt_store16(reinterpret_cast<uint8_t*>(rew) + o, *reinterpret_cast<const u32x4*>(tr + r * EPW + c));
             if (flg) nt_store16(flg + o, *reinterpret_cast<const u32x4*>(tf + r * EPW + c));
+            if constexpr (RULES) {   // the tile's rule bits: whole 16-B pieces of each step's EPW-env run
+                constexpr uint32_t kPer = EPW / 8, kPieces = kTile * kPer;   // 16-B pieces per row / tile
+#pragma unroll
+                for (uint32_t pi = lane; pi < kPieces; pi += 64) {
+                    const uint32_t row = pi / kPer, col = (pi % kPer) * 8;
+                    nt_store16(reinterpret_cast<uint8_t*>(rtr.bits + (size_t)(tb + row) * n + wave_base + col),
+                               *reinterpret_cast<const u32x4*>(tbits + row * EPW + col));
+                }
+            }
             wave_lds_fence();
         } else if (active || OBS) {
             for (int k = 0; k < cnt; ++k) {
@@ -443,7 +457,7 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
                     acc.y += (f & 3u) ? 1 : 0;
                     acc.z += ((f & 3u) && code == 100) ? 1 : 0;
                     acc.w += (f & 64u) ? 1 : 0;
-                    audit_step(t);
+                    audit_step(t, rtr.bits + (size_t)t * n + i);
                 }
                 obs(t);
             }
@@ -1632,7 +1646,8 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
     int lds_rc = SPARC_OK;   // allow_big_lds failure inside a launch lambda (then no launch)
     int4* st = reinterpret_cast<int4*>(d_stats);
     auto aligned = [](const void* q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & 15u) == 0; };
-    const uint32_t tiled = (c->n % 16 == 0) && aligned(d_act) && aligned(d_rew) && aligned(d_flags);
+    const uint32_t tiled = (c->n % 16 == 0) && aligned(d_act) && aligned(d_rew) && aligned(d_flags) &&
+                           (!rtr || aligned(rtr->bits));
     // the puzzle rows are staged in LDS when they fit next to the I/O tiles without costing
     // occupancy: budget = LDS per CU / resident workgroups per CU (256 CUs)
     // envs per wave: 64.  (Measured on MI355X at 65,536 envs: 32-wide waves, two per SIMD, are
@@ -1746,7 +1761,8 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
             const size_t blocks = (c->n + kWaves * EPW - 1) / (kWaves * EPW);
             const size_t per_cu = (blocks + 255) / 256;
             const size_t budget = std::min(kMaxDynLds, (size_t)160 * 1024 / (per_cu ? per_cu : 1));
-            const size_t base = tiles_lds_bytes<W, EPW>() + stack_lds_bytes<W, TB, EPW>() + (OBS ? obs_lds_bytes<W>() : 0);
+            const size_t base = tiles_lds_bytes<W, EPW>() + stack_lds_bytes<W, TB, EPW>() + (OBS ? obs_lds_bytes<W>() : 0) +
+                                (RULES ? bits_lds_bytes<EPW>() : 0);
             const size_t tbytes = table_lds_bytes<W>(c->num_puzzles);
             const bool lds_table = base + tbytes <= budget;
             const size_t shm = base + (lds_table ? tbytes : 0);

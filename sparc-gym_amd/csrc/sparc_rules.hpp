@@ -107,11 +107,19 @@ struct BB {
     }
 };
 
+// the puzzle's instance list and shapes for the exact fit, by value (the search is a call: a
+// pointer to a kernel-argument table, or a reference to a region board, would put them in
+// scratch memory on every region)
 struct FitIn {
-    const RulesTab* rt;
+    const uint32_t* inst;
+    const uint32_t* shape_range;
+    const int8_t* shape_off;
     uint32_t first, count;   // the puzzle's instance range
     uint32_t CX, CY;         // cell grid
 };
+__device__ __forceinline__ FitIn fit_in(const RulesTab& rt, uint32_t ir, uint32_t X, uint32_t Y) {
+    return FitIn{rt.inst, rt.shape_range, rt.shape_off, ir & 0xFFFFu, ir >> 16, (X - 1) / 2, (Y - 1) / 2};
+}
 
 // ---------------------------------------------------------------- exact fit (736-838)
 // The search runs on the cell grid (CX x CY <= 7 x 7 cells, bit cx*CY + cy of a u64: the
@@ -142,7 +150,7 @@ struct FitGrid {
 };
 
 // pattern (relative to the anchor) and fitting anchors of shape `sh` on a CX x CY cell grid
-__device__ __forceinline__ void fit_shape(const RulesTab& rt, uint32_t sh, uint32_t CX, uint32_t CY, uint64_t& pat,
+__device__ __forceinline__ void fit_shape(const FitIn& rt, uint32_t sh, uint32_t CX, uint32_t CY, uint64_t& pat,
                                           uint64_t& va) {
     const uint32_t sr = rt.shape_range[sh];
     const uint32_t o0 = sr & 0xFFFFu, n = sr >> 16;
@@ -210,8 +218,8 @@ __device__ __forceinline__ uint64_t cell_mask_p8(const FitIn& in, uint64_t rc) {
 // then reports SPARC_RULE_SEARCH_EXHAUSTED; the reference would keep searching).  rm: the
 // region's cells (cell_mask).
 template <int W>
-__device__ __noinline__ int exact_fit(const FitIn& in, const BB<W>& Rc, uint64_t rm) {
-    const RulesTab& rt = *in.rt;
+__device__ __noinline__ int exact_fit(const FitIn in, const BB<W> Rc, uint64_t rm) {
+    const FitIn& rt = in;
     const uint32_t CX = in.CX, CY = in.CY;
     FitGrid g;
 #pragma unroll
@@ -420,7 +428,7 @@ __device__ uint32_t region_table_word(const Params& p, const RulesTab& rt, uint3
     const uint4 inf = p.tab.info[q];
     const uint32_t X = inf.x & 0xFFu, Y = (inf.x >> 8) & 0xFFu;
     const uint32_t ir = rt.inst_range[q];
-    const FitIn fin{&rt, ir & 0xFFFFu, ir >> 16, (X - 1) / 2, (Y - 1) / 2};
+    const FitIn fin = fit_in(rt, ir, X, Y);
     const uint32_t cells = fin.CX * fin.CY;
     BB<W> pl[RP_ABI];
     const uint64_t* gp = rt.planes + (size_t)q * RP_COUNT * W;
@@ -469,7 +477,7 @@ __device__ __forceinline__ PuzzleRules<W> puzzle_rules(const Params& p, const Ru
     r.fo = rt.reg_off ? rt.reg_off[q] : kNoRegTab;
     r.tx = inf.y & 0xFFu;
     r.ty = (inf.y >> 8) & 0xFFu;
-    r.fin = FitIn{&rt, ir & 0xFFFFu, ir >> 16, (X - 1) / 2, (Y - 1) / 2};
+    r.fin = fit_in(rt, ir, X, Y);
     return r;
 }
 
