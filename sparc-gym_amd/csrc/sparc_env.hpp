@@ -51,6 +51,7 @@ struct Table {
     const uint4* __restrict__ row1;     // [P] padded W = 1 layout: compact puzzle row
     const uint4* __restrict__ trie1;    // [nodes] W = 1 layout: packed nodes (see Env<1>)
     const uint2* __restrict__ trie8;    // [nodes] split-kernel trie records (sparc_trie.hpp)
+    const uint2* __restrict__ trieg;    // [nodes][4] record of each node's field-d node (TrieLane::step1la)
     const uint4* __restrict__ trow;     // [P] split-kernel trie rows (sparc_trie.hpp)
     const uint4* __restrict__ mrow;     // [P] W = 1 split move wave: {row1.x, reset board lo, hi, 0}
     uint32_t num_puzzles;

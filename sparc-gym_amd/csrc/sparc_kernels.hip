@@ -689,7 +689,7 @@ __device__ __forceinline__ uint32_t flag_bytes4(const u32x4 w) {
     return lo | (hi << 16);
 }
 
-template <bool TB, bool RAND, bool LDS_TABLE>
+template <bool TB, bool RAND, bool LDS_TABLE, bool LA = false>
 __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, const uint8_t* __restrict__ act,
                                                         uint64_t seed, uint64_t t0, int8_t* __restrict__ rew,
                                                         uint8_t* __restrict__ flg, int4* __restrict__ stats) {
@@ -837,22 +837,36 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         tl.load(p.st.pos[i], p.st.aux[i], p.st.pid[i], trow, p.tab.trie8, NP);
         const uint32_t* th = reinterpret_cast<const uint32_t*>(pb + kS_FH) + lane;
         uint8_t* tr = pb + kS_Rew + lane;
+        static_assert(!(LA && RAND), "the look-ahead trie wave reads the next tile's actions from HBM tiles");
         __syncthreads();                                         // B_0
         __syncthreads();                                         // B_1 (interval 0: no tile yet)
+        if constexpr (LA)
+            if (K > 0) tl.prime(pb[kS_Act + lane], p.tab.trieg);   // step 0's action (tile 0, buffer 0)
         for (int32_t k = 1; k <= K; ++k) {
             const uint8_t* ta = pb + kS_Act + ((k - 1) % 3) * (kTile * 64) + lane;   // tile k-1's actions
+            // LA: tile k's first action is the look-ahead of tile k-1's last step; buffer k % 3
+            // holds tile k during this interval (loaded by the I/O wave in the last one; after
+            // the last tile it is stale, and that look-ahead is never used)
+            const uint32_t a_next = LA ? pb[kS_Act + (k % 3) * (kTile * 64) + lane] : 0u;
 #pragma unroll 1
             for (int g = 0; g < kTile; g += 4) {
-                // the group's 4 hand-over words and actions first (one LDS wait), then its 4 steps
+                // the group's 4 hand-over words and actions (LA: and the next one) first (one LDS
+                // wait), then its 4 steps
                 const uint32_t row0 = (uint32_t)((k - 1) * kTile + g) & (kRing - 1);
-                uint32_t hb[4], av[4];
+                uint32_t hb[4], av[5];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     hb[j] = th[(row0 + j) * 64];
                     av[j] = ta[(g + j) * 64];
                 }
+                if constexpr (LA) av[4] = g + 4 < kTile ? (uint32_t)ta[(g + 4) * 64] : a_next;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) tr[(row0 + j) * 64] = (uint8_t)tl.step1(hb[j], av[j], trow, p.tab.trie8, NP);
+                for (int j = 0; j < 4; ++j) {
+                    int code;
+                    if constexpr (LA) code = tl.step1la(hb[j], av[j], av[j + 1], trow, p.tab.trieg, NP);
+                    else code = tl.step1(hb[j], av[j], trow, p.tab.trie8, NP);
+                    tr[(row0 + j) * 64] = (uint8_t)code;
+                }
             }
             __syncthreads();                                     // B_{k+1}
         }
@@ -1082,6 +1096,7 @@ struct Ctx {
     uint64_t* t_init = nullptr;
     uint4* t_row1 = nullptr;
     uint2* t_trie8 = nullptr;          // split-kernel tables (null: a puzzle's trie exceeds 15-bit nodes)
+    uint2* t_trieg = nullptr;          // [nodes][4]: the record of each node's field-d node (k_rollout1s)
     uint4 *t_trow = nullptr, *t_mrow = nullptr;
     // multi-word split kernel (k_rolloutWs): move rows and reset boards; split_w false when the
     // pool does not fit its layout (pitch > 15, LDS, or no trie8)
@@ -1149,6 +1164,7 @@ Params make_params(const Ctx* c) {
     p.tab.init = c->t_init;
     p.tab.row1 = c->t_row1;
     p.tab.trie8 = c->t_trie8;
+    p.tab.trieg = c->t_trieg;
     p.tab.trow = c->t_trow;
     p.tab.mrow = c->t_mrow;
     p.tab.num_puzzles = c->num_puzzles;
@@ -1370,6 +1386,7 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
     if (c->t_init) HIPCHK(c, hipFree(c->t_init));
     if (c->t_row1) HIPCHK(c, hipFree(c->t_row1));
     if (c->t_trie8) HIPCHK(c, hipFree(c->t_trie8));
+    if (c->t_trieg) HIPCHK(c, hipFree(c->t_trieg));
     if (c->t_trow) HIPCHK(c, hipFree(c->t_trow));
     if (c->t_mrow) HIPCHK(c, hipFree(c->t_mrow));
     if (c->t_mroww) HIPCHK(c, hipFree(c->t_mroww));
@@ -1378,6 +1395,7 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
     c->t_boardw = nullptr;
     c->split_w = false;
     c->t_trie8 = nullptr;
+    c->t_trieg = nullptr;
     c->t_trow = nullptr;
     c->t_mrow = nullptr;
     c->t_init = nullptr;
@@ -1509,6 +1527,24 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
         }
         HIPCHK(c, hipMalloc(&c->t_trie8, sizeof(uint2) * nn));
         HIPCHK(c, hipMemcpy(c->t_trie8, t8.data(), sizeof(uint2) * nn, hipMemcpyHostToDevice));
+        // look-ahead records (TrieLane::step1la): entry 4k + d = the record of node k's field-d
+        // node (child, or the parent in the back direction), all ones where the field is empty;
+        // at least 4 entries, so that a rootless puzzle's lane (base 0, node 0) reads in bounds
+        std::vector<uint2> tg(4 * std::max<size_t>(nn, 1), make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu));
+        for (size_t q = 0; q < P; ++q) {
+            const uint32_t* inf = t->info + 4 * q;
+            if (!((inf[1] >> 16) & 2u)) continue;
+            const size_t base = inf[2];
+            const uint32_t cnt = inf[3] & 0xFFFFu;
+            for (uint32_t k = 0; k < cnt; ++k) {
+                const uint2 r = t8[base + k];
+                const uint32_t f[4] = {r.x & 0xFFFFu, r.x >> 16, r.y & 0xFFFFu, r.y >> 16};
+                for (int d = 0; d < 4; ++d)
+                    if (f[d] != 0xFFFFu) tg[4 * (base + k) + d] = t8[base + (f[d] & 0x7FFFu)];
+            }
+        }
+        HIPCHK(c, hipMalloc(&c->t_trieg, sizeof(uint2) * tg.size()));
+        HIPCHK(c, hipMemcpy(c->t_trieg, tg.data(), sizeof(uint2) * tg.size(), hipMemcpyHostToDevice));
         HIPCHK(c, hipMalloc(&c->t_trow, sizeof(uint4) * P));
         HIPCHK(c, hipMemcpy(c->t_trow, trow.data(), sizeof(uint4) * P, hipMemcpyHostToDevice));
         HIPCHK(c, hipMalloc(&c->t_mrow, sizeof(uint4) * P));
@@ -1673,7 +1709,9 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
             auto go_s = [&](auto tb) {
                 constexpr bool TB = decltype(tb)::value;
                 if (d_act) {
-                    if (lds_s) launch_s(k_rollout1s<TB, false, true>, d_act);
+                    // look-ahead trie gathers on grids of at most 64 workgroups (sparc_trie.hpp)
+                    if (lds_s && blocks <= 64) launch_s(k_rollout1s<TB, false, true, true>, d_act);
+                    else if (lds_s) launch_s(k_rollout1s<TB, false, true>, d_act);
                     else launch_s(k_rollout1s<TB, false, false>, d_act);
                 } else {
                     if (lds_s) launch_s(k_rollout1s<TB, true, true>, nullptr);

@@ -65,8 +65,7 @@ struct MoveLane1 {
     uint32_t sp = 0, bks = 0, bias = 0;   // traceback: stack slot len-1 (LDS byte address), rule bias
     uint32_t rp = 0, pnr = 0;             // traceback: back position of the last move / the one before
     uint32_t lv = 0x30000u;               // flag-bit mask of the step: term | trunc, or kHwReset
-    uint32_t rpid = 0, rrow = 0;          // the next autoreset's row word and the puzzle after it
-    uint64_t rinit = 0;                   // ... and its free board
+    uint4 rr = {0u, 0u, 0u, 0u};          // the next autoreset's move row: row word, free board, the puzzle after it
 
     typedef __attribute__((address_space(3))) uint8_t lds_u8;
     __device__ __forceinline__ static lds_u8* lds_byte(uint32_t a) { return (lds_u8*)(uintptr_t)a; }
@@ -77,26 +76,22 @@ struct MoveLane1 {
         bks = 0x80000000u - col_addr - 128u + 64u * ((~pflags >> 2) & 1u);
     }
     __device__ __forceinline__ void prefetch_reset(const uint4* mrow, uint32_t q) {
-        const uint4 m = mrow[q];
-        rrow = m.x;
-        rinit = ((uint64_t)m.z << 32) | m.y;
-        rpid = m.w;
+        rr = mrow[q];
     }
 
     // gymnasium next-step autoreset (reset(), SPaRC_Gym.py:1087): the next puzzle's row and
     // board from registers (read at the previous reset); the step then moves nowhere (w = 0,
     // bias = 0) and reports the reset flag instead of term / trunc (lv).  The row of the reset
-    // after it is read on every step, outside the branch: read inside, the branch waits for it
-    // (it lands in temporaries and is copied on), and about a fifth of all wave-steps take the
-    // branch (MI355X, per-role stamps of tools/diag_split.py: the move wave's step 421.8 ->
-    // 409.3 cycles at 65,536 envs)
+    // after it is read inside the branch straight into the same registers, so nothing waits for
+    // it until the next reset (at least two steps later: a reset step is never done).  Copied
+    // on from temporaries instead, the branch waited for the LDS read on every reset (about a
+    // fifth of all wave-steps take the branch)
     __device__ __forceinline__ void reset_next(const Params& p, const uint4* mrow, uint32_t col_addr) {
-        const uint4 nx = mrow[rpid];
         if ((pending != 0u) & (p.autoreset == 1)) {
-            e = rrow & 0xFFu;
-            tgt = (rrow >> 8) & 0xFFu;
-            pflags = rrow >> 16;
-            fr = rinit;
+            e = rr.x & 0xFFu;
+            tgt = (rr.x >> 8) & 0xFFu;
+            pflags = rr.x >> 16;
+            fr = ((uint64_t)rr.z << 32) | rr.y;
             w = 0;
             if constexpr (TB) {
                 sp = col_addr;   // len = 1
@@ -107,9 +102,7 @@ struct MoveLane1 {
             }
             step = -1;   // this step's increment brings it to 0
             lv = kHwReset;
-            rrow = nx.x;
-            rinit = ((uint64_t)nx.z << 32) | nx.y;
-            rpid = nx.w;
+            rr = mrow[rr.w];
         }
     }
 

@@ -72,6 +72,71 @@ struct TrieLane {
         nx = trow[npid];
     }
 
+    // ---- look-ahead form (k_rollout1s on small grids).  The trie wave runs a tile behind the
+    // move wave, so it knows the NEXT step's action too.  After each step it gathers, from trieg
+    // (entry 4k + d = the record of node k's field-d node), the record the next step moves to IF
+    // it moves along the trie: one unconditional 8-B gather per step whose data is used a whole
+    // step later (the plain form's gather of the new node's own record is used half a step
+    // later).  It pays only while the L2 is lightly loaded (MI355X, 2,000-step launches: c2 at
+    // 4,096 envs 0.350 -> 0.337 ms; c3 at 65,536 envs 0.392 -> 0.410 ms, as 65,536 lanes then
+    // gather every step instead of on the rare node changes), so the host uses it for grids of
+    // at most 64 workgroups.
+    uint32_t nrx = ~0u, nry = ~0u;  // record of field[a] of the current node (a = this step's action)
+
+    // after load(): the first step's look-ahead record (a0: its action)
+    __device__ __forceinline__ void prime(const uint32_t a0, const uint2* __restrict__ trieg) {
+        const uint32_t node = S & 0x7FFFu;
+        const uint2 rec = trieg[((base + (node < tmax ? node : tmax)) << 2) + (a0 & 3u)];
+        nrx = rec.x;
+        nry = rec.y;
+    }
+
+    // step1 (the W = 1 move wave's word) with the look-ahead record; an: the next step's action
+    template <class Rows>
+    __device__ __forceinline__ int step1la(const uint32_t hw, const uint32_t a, const uint32_t an, const Rows& trow,
+                                           const uint2* __restrict__ trieg, uint32_t num_puzzles) {
+        const bool reset = (hw & 0x400000u) != 0u;
+        const uint32_t dd = (uint32_t)((int32_t)hw >> 14) & 0xFFFF0000u;
+        const bool moved = hw >= 0x40000000u;
+        const bool done = (hw & 0x30000u) != 0u;
+        if (reset) {
+            pid = npid;
+            npid = next_pid(npid, num_puzzles);
+            rx = nx.x;
+            ry = nx.y;
+            base = nx.z;
+            S = nx.w & 0x18000u;
+            hs = (int32_t)((nx.w >> 14) & 1u);
+            hsn = -hs;
+            tmax = nx.w >> 17;
+        }
+        nx = trow[npid];
+        const uint64_t xy = ((uint64_t)ry << 32) | rx;
+        const uint32_t c = (uint32_t)(xy >> ((a << 4) & 0x30u));
+        const uint32_t key = __builtin_amdgcn_ubfe(c, 0u, 16u) | (S & 0xFFFF0000u) | (~dd & 0x10000u);
+        const bool take = key < 0xFFFFu;
+        S = take ? key : S + dd;
+        // the new node's record arrived with the previous step's look-ahead gather (a reset
+        // step never takes: dd = 0)
+        rx = take ? nrx : rx;
+        ry = take ? nry : ry;
+        // the next step's: field[an] of the node now current (on or off the trie, the node is
+        // one of this puzzle's: in bounds; used only if that step takes).  Unconditional: an
+        // exec-masked gather for on-trie lanes only measured slower here (c2: 0.346 vs 0.337 ms)
+        const uint2 rec = trieg[((base + (S & 0x7FFFu)) << 2) + (an & 3u)];
+        nrx = rec.x;
+        nry = rec.y;
+        const uint32_t x = S >> 15;
+        const int cd = x == 1u ? 100 : Oneg;
+        const int cm = moved ? (x < 2u ? hs : hsn) : 0;
+        const int code = done ? cd : cm;
+        Oneg = done ? (cd < 0 ? cd : 0) : -100;
+        acc_x += code;
+        acc_y += (uint32_t)done;
+        acc_z += (uint32_t)(code == 100);
+        return code;
+    }
+
     // one env-step from its hand-over word (layout above) and action; returns the reward code
     // (x100, 1201-1223)
     template <class Rows>

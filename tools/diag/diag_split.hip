@@ -75,10 +75,10 @@ struct DiagMoveLane1 : MoveLane1<TB> {
             if (__builtin_amdgcn_ballot_w64((B::pending != 0u) & (p.autoreset == 1))) B::reset_next(p, mrow, col_addr);
         } else if constexpr (MV == 4) {   // the branch without the next-row prefetch (timing only)
             if ((B::pending != 0u) & (p.autoreset == 1)) {
-                B::e = B::rrow & 0xFFu;
-                B::tgt = (B::rrow >> 8) & 0xFFu;
-                B::pflags = B::rrow >> 16;
-                B::fr = B::rinit;
+                B::e = B::rr.x & 0xFFu;
+                B::tgt = (B::rr.x >> 8) & 0xFFu;
+                B::pflags = B::rr.x >> 16;
+                B::fr = ((uint64_t)B::rr.z << 32) | B::rr.y;
                 B::w = 0;
                 if constexpr (TB) {
                     B::sp = col_addr;
@@ -91,12 +91,12 @@ struct DiagMoveLane1 : MoveLane1<TB> {
                 B::lv = kHwReset;
             }
         } else if constexpr (MV == 5) {   // the next-row prefetch every step, outside the branch
-            const uint4 nx = mrow[B::rpid];
+            const uint4 nx = mrow[B::rr.w];
             if ((B::pending != 0u) & (p.autoreset == 1)) {
-                B::e = B::rrow & 0xFFu;
-                B::tgt = (B::rrow >> 8) & 0xFFu;
-                B::pflags = B::rrow >> 16;
-                B::fr = B::rinit;
+                B::e = B::rr.x & 0xFFu;
+                B::tgt = (B::rr.x >> 8) & 0xFFu;
+                B::pflags = B::rr.x >> 16;
+                B::fr = ((uint64_t)B::rr.z << 32) | B::rr.y;
                 B::w = 0;
                 if constexpr (TB) {
                     B::sp = col_addr;
@@ -107,30 +107,29 @@ struct DiagMoveLane1 : MoveLane1<TB> {
                 }
                 B::step = -1;
                 B::lv = kHwReset;
-                B::rrow = nx.x;
-                B::rinit = ((uint64_t)nx.z << 32) | nx.y;
-                B::rpid = nx.w;
+                B::rr = nx;
             }
         } else if constexpr (MV == 3) {
             const bool rs = (B::pending != 0u) & (p.autoreset == 1);
-            const uint4 nx = mrow[B::rpid];
-            B::e = rs ? (B::rrow & 0xFFu) : B::e;
-            B::tgt = rs ? ((B::rrow >> 8) & 0xFFu) : B::tgt;
-            B::pflags = rs ? (B::rrow >> 16) : B::pflags;
-            B::fr = rs ? B::rinit : B::fr;
+            const uint4 nx = mrow[B::rr.w];
+            B::e = rs ? (B::rr.x & 0xFFu) : B::e;
+            B::tgt = rs ? ((B::rr.x >> 8) & 0xFFu) : B::tgt;
+            B::pflags = rs ? (B::rr.x >> 16) : B::pflags;
+            B::fr = rs ? (((uint64_t)B::rr.z << 32) | B::rr.y) : B::fr;
             B::w = rs ? 0u : B::w;
             if constexpr (TB) {
                 B::sp = rs ? col_addr : B::sp;
-                B::bks = rs ? 0x80000000u - col_addr - 128u + 64u * ((~(B::rrow >> 16) >> 2) & 1u) : B::bks;
+                B::bks = rs ? 0x80000000u - col_addr - 128u + 64u * ((~(B::rr.x >> 16) >> 2) & 1u) : B::bks;
                 B::bias = rs ? 0u : B::bias;
             } else {
                 B::len = rs ? 1u : B::len;
             }
             B::step = rs ? -1 : B::step;
             B::lv = rs ? kHwReset : B::lv;
-            B::rrow = rs ? nx.x : B::rrow;
-            B::rinit = rs ? (((uint64_t)nx.z << 32) | nx.y) : B::rinit;
-            B::rpid = rs ? nx.w : B::rpid;
+            B::rr.x = rs ? nx.x : B::rr.x;
+            B::rr.y = rs ? nx.y : B::rr.y;
+            B::rr.z = rs ? nx.z : B::rr.z;
+            B::rr.w = rs ? nx.w : B::rr.w;
         }
     }
 };
