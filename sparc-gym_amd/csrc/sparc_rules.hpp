@@ -524,9 +524,17 @@ __device__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const PuzzleRul
         R.set(remaining.lowest());
         while (true) {                                           // flood fill (BFS 431-452)
             BB<W> N;
-            if constexpr (W == 1)   // the padded one-word geometry: a y step off the lattice lands on a blocked bit
-                N = R | R.shl(1) | R.shr(1) | R.shl(P) | R.shr(P);
-            else
+            if constexpr (W == 1) {
+                // the padded one-word geometry: a y step off the lattice lands on a blocked bit,
+                // so each lattice row's runs of allowed bits end below a zero.  Toward +y the
+                // whole run above each bit of R (R within allowed) fills in one add: the carry
+                // from R ripples up through the run (the allowed bits it clears, plus the seeds,
+                // are the fill).  -y and +-x stay one step per iteration.  Flood iterations per
+                // 64-env wave-step (c3 pool, random walks, regions run in lock step): 39.9 -> 34.4
+                const uint64_t a = allowed.w[0], r = R.w[0];
+                const uint64_t up = (((a + r) ^ a) & a) | r;
+                N.w[0] = up | (r >> 1) | (r << P) | (r >> P);
+            } else
                 N = R | (R.shl(1) & nfirst) | (R.shr(1) & nlast) | R.shl(P) | R.shr(P);
             N = N & allowed;
             if (N == R) break;
