@@ -278,7 +278,13 @@ struct ObsTrace {
 };
 // RULES: after every step the wave also runs the rule audit of every env's new state
 // (_validate_rules, which the reference's step() runs every step, SPaRC_Gym.py:1227 / 1011) and
-// writes its bits to bits + t * N ([T][N] uint16, as sparc_rules_device's bits)
+// writes its bits to bits + t * N ([T][N] uint16, as sparc_rules_device's bits).  A rule
+// rollout runs TWO waves per EPW envs (waves 2j and 2j+1 of a workgroup): both step the same envs
+// (the step is deterministic and ~1/7 of the work), wave parity q audits the steps t with
+// t % 2 == q, and only wave 0 of the pair writes the rewards, flags, stats, state and memo.  The
+// audit is a latency-bound chain (flood fills, table lookups; ~40 % of its cycles waiting at one
+// wave per SIMD); two per SIMD interleave (MI355X, c3r at 65,536 envs: see DESIGN.md §5)
+constexpr uint32_t kAuditWaves = 2;   // waves per EPW envs in a rule rollout (a divisor of kWaves and kTile)
 struct RuleTrace {
     RulesTab rt;
     uint16_t* bits;
@@ -333,7 +339,11 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
             src = PuzzleSrc<W>{linfo, lroot, lopen, p.tab.init, p.tab.row1};
         }
     }
-    const uint32_t wave_base = (blockIdx.x * kWaves + wv) * EPW;
+    // RULES: wave pairs on the same envs (above); q = the steps this wave audits (t % 2 == q)
+    constexpr uint32_t kPerEnv = RULES ? kAuditWaves : 1u;
+    const uint32_t q = RULES ? (wv % kAuditWaves) : 0u;
+    const bool lead = q == 0u;   // writes the outputs, stats, state and memo
+    const uint32_t wave_base = (blockIdx.x * (kWaves / kPerEnv) + wv / kPerEnv) * EPW;
     if (wave_base >= p.n || lane >= (uint32_t)EPW) return;   // no block-level barrier after here
     const uint32_t i = wave_base + lane;
     const bool active = i < p.n;
@@ -370,6 +380,7 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
         if (rtr.memo && i < p.n) memo = rtr.memo[i];
     auto audit_step = [&](int32_t t, uint16_t* slot) {   // rule bits of the state after step t -> slot
         if constexpr (RULES) {
+            if ((uint32_t)t % kAuditWaves != q) return;   // a partner wave's step (wave-uniform)
             uint64_t v[W];
             uint32_t ab;
             e.obs_words(p, src, v, ab);
@@ -432,13 +443,16 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
             }
             wave_lds_fence();
             const size_t o = (size_t)(tb + r) * n + wave_base + c;
-            if (rew) nt_store16(reinterpret_cast<uint8_t*>(rew) + o, *reinterpret_cast<const u32x4*>(tr + r * EPW + c));
-            if (flg) nt_store16(flg + o, *reinterpret_cast<const u32x4*>(tf + r * EPW + c));
-            if constexpr (RULES) {   // the tile's rule bits: whole 16-B pieces of each step's EPW-env run
-                constexpr uint32_t kPer = EPW / 8, kPieces = kTile * kPer;   // 16-B pieces per row / tile
+            if (lead) {
+                if (rew) nt_store16(reinterpret_cast<uint8_t*>(rew) + o, *reinterpret_cast<const u32x4*>(tr + r * EPW + c));
+                if (flg) nt_store16(flg + o, *reinterpret_cast<const u32x4*>(tf + r * EPW + c));
+            }
+            if constexpr (RULES) {   // the tile's rule bits of this wave's steps (rows t % 2 == q; tb is even):
+                                     // whole 16-B pieces of each step's EPW-env run
+                constexpr uint32_t kPer = EPW / 8, kPieces = kTile / kAuditWaves * kPer;   // 16-B pieces per row / this wave's rows
 #pragma unroll
                 for (uint32_t pi = lane; pi < kPieces; pi += 64) {
-                    const uint32_t row = pi / kPer, col = (pi % kPer) * 8;
+                    const uint32_t row = kAuditWaves * (pi / kPer) + q, col = (pi % kPer) * 8;
                     nt_store16(reinterpret_cast<uint8_t*>(rtr.bits + (size_t)(tb + row) * n + wave_base + col),
                                *reinterpret_cast<const u32x4*>(tbits + row * EPW + col));
                 }
@@ -451,8 +465,8 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
                     const uint32_t a = RAND ? uint_rand_action(seed, gid, t0 + (uint64_t)t) : act[(size_t)t * n + i];
                     uint32_t f;
                     const int code = e.advance(p, src, a, f);
-                    if (rew) rew[(size_t)t * n + i] = (int8_t)code;
-                    if (flg) flg[(size_t)t * n + i] = (uint8_t)f;
+                    if (rew && lead) rew[(size_t)t * n + i] = (int8_t)code;
+                    if (flg && lead) flg[(size_t)t * n + i] = (uint8_t)f;
                     acc.x += code;
                     acc.y += (f & 3u) ? 1 : 0;
                     acc.z += ((f & 3u) && code == 100) ? 1 : 0;
@@ -463,7 +477,7 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
             }
         }
     }
-    if (!active) return;
+    if (!active || !lead) return;
     e.store(p, src, i);
     if constexpr (RULES)
         if (rtr.memo) rtr.memo[i] = memo;
@@ -1796,7 +1810,8 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
             constexpr bool OBS = decltype(obs_c)::value;
             constexpr bool RULES = decltype(rules_c)::value;
             if constexpr (W == 1 && !OBS && !RULES) return;   // k_rollout1 above
-            const size_t blocks = (c->n + kWaves * EPW - 1) / (kWaves * EPW);
+            constexpr size_t kEnvsPerBlock = (size_t)kWaves * EPW / (RULES ? kAuditWaves : 1);   // RULES: wave groups
+            const size_t blocks = (c->n + kEnvsPerBlock - 1) / kEnvsPerBlock;
             const size_t per_cu = (blocks + 255) / 256;
             const size_t budget = std::min(kMaxDynLds, (size_t)160 * 1024 / (per_cu ? per_cu : 1));
             const size_t base = tiles_lds_bytes<W, EPW>() + stack_lds_bytes<W, TB, EPW>() + (OBS ? obs_lds_bytes<W>() : 0) +
