@@ -164,6 +164,44 @@ def test_rollout_rule_bits_every_step(on_gpu, sizes, max_shaped):
     assert len(np.unique(bits)) > 4
 
 
+@pytest.mark.parametrize("n", [200, 1000, 1040])
+def test_rollout_rule_bits_ragged_batches(on_gpu, n):
+    """Rule rollouts over batches that are not whole workgroups (two audit waves per 64 envs, each
+    auditing every other step): 200 and 1000 envs (not multiples of 16: every step goes through the
+    per-step path), 1040 (tiled, with a last wave pair of 16 envs), an odd T split over two
+    launches; the bits after every step equal step()-by-step() audits and the reward codes /
+    flags / stats equal a plain rollout's."""
+    from sparc_gym_amd import SPaRCVecEnv, synthetic
+    from sparc_gym_amd.puzzles import process_puzzles
+    recs = synthetic.make_rule_puzzles(96, seed=5, sizes=((3, 3),), break_prob=0.3)
+    recs += synthetic.make_puzzles(96, seed=6, sizes=((3, 3),), full_properties=True)
+    proc = process_puzzles(recs)
+    T1, T2 = 21, 16
+    kw = dict(processed=proc, traceback=True, autoreset="next_step", observation="compact", rules=True,
+              max_steps=9)
+    pids = (np.arange(n) * 29) % len(proc)
+    acts = torch.randint(0, 5, (T1 + T2, n), dtype=torch.uint8, device="cuda")
+    a = SPaRCVecEnv(n, **kw)
+    a.reset(options={"puzzle_index": pids})
+    sa = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
+    r1 = a.rollout(T1, acts[:T1], rules=True, stats=sa)
+    r2 = a.rollout(T2, acts[T1:], rules=True, stats=sa)
+    b = SPaRCVecEnv(n, **kw)
+    b.reset(options={"puzzle_index": pids})
+    sb = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
+    rb = b.rollout(T1 + T2, acts, stats=sb)
+    assert torch.equal(torch.cat([r1["reward_code"], r2["reward_code"]]), rb["reward_code"])
+    assert torch.equal(torch.cat([r1["flags"], r2["flags"]]), rb["flags"])
+    assert torch.equal(sa, sb)
+    bits = torch.cat([r1["rule_bits"], r2["rule_bits"]]).cpu().numpy()
+    c = SPaRCVecEnv(n, **kw)
+    c.reset(options={"puzzle_index": pids})
+    for t in range(T1 + T2):
+        _, _, _, _, info = c.step(acts[t])
+        assert np.array_equal(bits[t], info["rule_bits"].cpu().numpy()), t
+    assert len(np.unique(bits)) > 4
+
+
 def test_rollout_rules_c3r_full_size(on_gpu):
     """The bench's c3r workload (bench.py --config c3r): 65,536 envs of the c3 pool, traceback,
     next-step autoreset, uint8 actions in HBM, the audit after every step inside the rollout
