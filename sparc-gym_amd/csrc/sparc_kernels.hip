@@ -971,6 +971,7 @@ __global__ void __launch_bounds__(kBlock1s) k_rolloutWs(Params p, SplitGeom g, c
         m.bd = reinterpret_cast<uint32_t*>(pb + g.off_board) + lane;
         m.col = pb + g.off_stack + lane;
         m.template load<W>(p, g, mrow, i);
+        m.prefetch_next(p, g, mrow, boards);
         const uint32_t pend0 = m.pending;
         const uint64_t gid = p.env_offset + i;
         uint16_t* th = reinterpret_cast<uint16_t*>(pb + kW_Hand) + lane;
@@ -1583,7 +1584,8 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
             g.off_board = (uint32_t)kW_Board;
             g.off_stack = g.off_board + g.BS * 256u;
             g.pair = (g.off_stack + g.M * 64u + 15u) & ~15u;
-            if (4 * (size_t)g.pair + splitw_fin_bytes() <= kMaxDynLds) {
+            // the move wave keeps the next reset board in kBoardRegs 16-B registers
+            if (4 * (size_t)g.pair + splitw_fin_bytes() <= kMaxDynLds && g.BS <= 4u * kBoardRegs) {
                 std::vector<uint4> mw(P);
                 std::vector<uint32_t> bw(P * g.BS, 0u);
                 for (size_t q = 0; q < P; ++q) {

@@ -49,6 +49,8 @@ __device__ __forceinline__ uint32_t widen_hand_word(uint32_t h) {
     return (h & 0xFFu) | ((__builtin_amdgcn_ubfe(h, 8u, 2u) - 1u) << 16);
 }
 
+constexpr uint32_t kBoardRegs = 4;   // 16-B pieces of the next reset board kept in registers
+
 template <bool TB>
 struct MoveLaneW {
     uint32_t e = 0, tgt = 0, len = 1, pflags = 0, bk = 0, legal = 0, rl = 0, pnr = 0, rs = 0, pending = 0, pid = 0;
@@ -57,6 +59,11 @@ struct MoveLaneW {
     uint32_t* bd = nullptr;          // this lane's dword 0 (stride 64 dwords)
     uint8_t* col = nullptr;          // this lane's stack column (stride 64 bytes)
     uint32_t s_a = 0, s_fwd = 0, s_pop = 0, s_mv = 0, s_done = 0;
+    // the next autoreset's move row and reset board (puzzle pid + 1), read at the previous reset
+    // (or at load) into registers: the reset then writes them to the LDS board without a memory
+    // round trip in the branch (BS <= kBoardRegs * 4 dwords, host-checked)
+    uint4 nrow = {0u, 0u, 0u, 0u};
+    uint4 nb[kBoardRegs];
 
     __device__ __forceinline__ uint32_t& dw(uint32_t k) const { return bd[k * 64u]; }
 
@@ -84,22 +91,37 @@ struct MoveLaneW {
     // gymnasium next-step autoreset (reset(), SPaRC_Gym.py:1087): puzzle index + 1 mod P, its
     // reset board copied into this lane's board.  Resets are rare per lane; the row and board
     // come from the L2-resident tables.
+    __device__ __forceinline__ void prefetch_next(const Params& p, const SplitGeom& g, const uint4* __restrict__ mrow,
+                                                  const uint32_t* __restrict__ boards) {
+        const uint32_t q = pid + 1 == p.tab.num_puzzles ? 0u : pid + 1;
+        nrow = mrow[q];
+        const uint4* src = reinterpret_cast<const uint4*>(boards + (size_t)q * g.BS);
+#pragma unroll
+        for (uint32_t k = 0; k < kBoardRegs; ++k)
+            if (4u * k < g.BS) nb[k] = src[k];
+    }
     __device__ __forceinline__ void reset_next(const Params& p, const SplitGeom& g, const uint4* __restrict__ mrow,
                                                const uint32_t* __restrict__ boards) {
         if (pending & (uint32_t)(p.autoreset == 1)) {
             pid = pid + 1 == p.tab.num_puzzles ? 0u : pid + 1;
-            apply_row(mrow[pid]);
-            const uint4* src = reinterpret_cast<const uint4*>(boards + (size_t)pid * g.BS);
-            for (uint32_t k = 0; k < g.BS; k += 4) {
-                const uint4 v = src[k >> 2];
-                dw(k) = v.x;
-                dw(k + 1u) = v.y;
-                dw(k + 2u) = v.z;
-                dw(k + 3u) = v.w;
+            apply_row(nrow);
+#pragma unroll
+            for (uint32_t k = 0; k < kBoardRegs; ++k) {
+                if (4u * k < g.BS) {
+                    dw(4u * k) = nb[k].x;
+                    dw(4u * k + 1u) = nb[k].y;
+                    dw(4u * k + 2u) = nb[k].z;
+                    dw(4u * k + 3u) = nb[k].w;
+                }
             }
             len = 1;
             step = -1;   // this step's increment brings it to 0
             rs = 1;
+            // the row's uses above happen before the reads below (memory clobber), so the reads
+            // can land in the same registers: copied on from temporaries instead, the branch
+            // would wait for them
+            asm volatile("" ::"v"(e), "v"(tgt), "v"(bk) : "memory");
+            prefetch_next(p, g, mrow, boards);   // waited for at the next reset
         }
     }
 
