@@ -5,7 +5,9 @@ Workload (default, BASELINE.json configs[2]): 65,536 concurrent 7x7 SPaRC instan
 full property set, traceback=True, max_steps=2000, gymnasium next-step autoreset onto the next
 puzzle, 1,024 synthetic puzzles (seed 0), env i -> puzzle (i * 2654435761) mod 1024.
 Actions are uniform random in {0,1,2,3}, generated on the GPU before the timed region (uint8
-tiles resident in HBM, like a policy's output).
+tiles resident in HBM, like a policy's output) by the counter-based generator keyed by the
+global env id (sparc_random_actions_device), so N ranks hold the tiles of one process over all
+N x envs and a sharded run equals the single-process one env for env.
 
 One bench "step" is one pass of the hot path over the batch: one rollout launch that advances
 every env by ``--env-steps`` T env.step()s (default 2,000; 50 for c4, whose launch also writes
@@ -65,6 +67,7 @@ CONFIGS = {
     "c3r": (((3, 3),), True, True, False),
 }
 RULE_CONFIGS = ("c3r",)
+ACTION_SEED = 1234   # seed of the bench's random action tiles (sparc_rand_action)
 DEFAULT_ENVS = {"c2": 4096, "c3": 65536, "c4": 262144, "c4c": 262144, "c3g7": 65536, "c3r": 65536}
 
 
@@ -87,7 +90,28 @@ def parse():
     ap.add_argument("--max-steps", type=int, default=2000)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    return ap.parse_args()
+    ap.add_argument("--stats-out", default="",
+                    help="rank 0 saves the gathered per-env stats [world*N, 4] int32 here (.npy; tests)")
+    a = ap.parse_args()
+    if a.mode == "step" and a.config in RULE_CONFIGS:
+        ap.error(f"--mode step runs no rule audit: {a.config} needs --mode rollout")
+    return a
+
+
+def rule_rollout_kernel(proc, table):
+    """The kernel sparc_rollout_rules_device runs on this pool (csrc rollout_impl): k_rollout1r
+    when the boards are one word, fit its ring word (x_size * pitch <= 57) and every puzzle has a
+    region-code table (at most 12 cells, 2^(cells) entries each within the 2^28-entry budget);
+    else the generic k_rollout<..., RULES>."""
+    if table.words != 1 or os.environ.get("SPARC_RULE_ROLLOUT") == "generic":
+        return "k_rollout"
+    entries = 0
+    for p in proc:
+        cells = ((p["x_size"] - 1) // 2) * ((p["y_size"] - 1) // 2)
+        if cells > 12 or p["x_size"] * table.pitch > 57:
+            return "k_rollout"
+        entries += 8 * (1 if cells <= 3 else 1 << (cells - 3))
+    return "k_rollout1r" if entries <= 1 << 28 else "k_rollout"
 
 
 def state_bytes_per_env(words, traceback):
@@ -98,38 +122,54 @@ def state_bytes_per_env(words, traceback):
 
 def cpu_baseline_rules(proc, tb, max_steps, seconds):
     """The reference-speed full step() including its rule audit: oracle/cpu_ref.py's step core +
-    oracle/rules_ref.py's _validate_rules restatement once per step (the reference runs it twice,
-    SPaRC_Gym.py:1227 and 1011), pure Python, 1 thread, random actions, next-step reset."""
+    oracle/rules_ref.py's _validate_rules restatement TWICE per step, as the reference runs it
+    (SPaRC_Gym.py:1227 with the step's flags, and 1011 in _get_info with both False), pure
+    Python, 1 thread, random actions.  Next-step autoreset as the GPU kernel counts it: the step
+    after a done step is the reset (reset() -> _load_puzzle 182 and _get_info 1011: two audits),
+    one env-step.  The rate with one audit per step is reported beside it."""
     from oracle.cpu_ref import CpuRefEnv
     from oracle import rules_ref
     pool = [{"x_size": p["x_size"], "y_size": p["y_size"], "start": list(p["start_location"]),
              "target": list(p["target_location"]), "solution_count": p["solution_count"],
              "solution_paths": p["solution_paths"], "gaps": p["obs_array"]["gaps"]} for p in proc]
     refp = [dict(p) for p in proc]
-    rng = np.random.default_rng(0)
-    q = 0
-    env = CpuRefEnv(pool[q], tb, max_steps)
-    k, t1 = 0, time.perf_counter()
-    while time.perf_counter() - t1 < seconds:
-        _, term, trunc = env.step(int(rng.integers(4)))
-        rules_ref.audit(refp[q], env.path, env.loc, term, trunc)
-        k += 1
-        if term or trunc:
-            q = (q + 1) % len(pool)
-            env.p = pool[q]
-            env.reset()
-    dt = time.perf_counter() - t1
+
+    def run(audits, secs):
+        rng = np.random.default_rng(0)
+        q = 0
+        env = CpuRefEnv(pool[q], tb, max_steps)
+        pending = False
+        k, t1 = 0, time.perf_counter()
+        while time.perf_counter() - t1 < secs:
+            if pending:                  # the autoreset step (its action is ignored)
+                q = (q + 1) % len(pool)
+                env.p = pool[q]
+                env.reset()
+                term = trunc = pending = False
+            else:
+                _, term, trunc = env.step(int(rng.integers(4)))
+                pending = term or trunc
+            rules_ref.audit(refp[q], env.path, env.loc, term, trunc)
+            if audits == 2:
+                rules_ref.audit(refp[q], env.path, env.loc, False, False)
+            k += 1
+        return k, time.perf_counter() - t1
+
+    k, dt = run(2, seconds)
+    k1, dt1 = run(1, min(seconds, 5.0))
     out = {"value": round(k / dt, 1), "unit": "env-steps/s", "cores": 1, "kind": "port",
-           "sample": f"oracle/cpu_ref.py step() + oracle/rules_ref.py rule audit once per step (pure Python, the "
-                     f"reference's algorithms), 1 env, {k} steps, random actions, {dt:.1f} s, 1 thread; CPU "
+           "sample": f"oracle/cpu_ref.py step() + oracle/rules_ref.py rule audit twice per step as the reference "
+                     f"(SPaRC_Gym.py:1227, 1011; pure Python, the reference's algorithms), 1 env, {k} steps incl. "
+                     f"next-step autoreset steps, random actions, {dt:.1f} s, 1 thread; CPU "
                      f"{platform.processor() or platform.machine()}, os.cpu_count()={os.cpu_count()}",
-           "value_1core": round(k / dt, 1)}
+           "value_1core": round(k / dt, 1),
+           "value_1core_audit_once": round(k1 / dt1, 1)}
     # the same on one process per core of this GPU's share of the host (BASELINE.md's plan)
     mp_ = _cpu_bench_multi("c3r", "py_rules", max_steps, seconds)
     if mp_:
         out.update(value=mp_["value"], cores=mp_["procs"],
                    sample=out["sample"] + f"; value: {mp_['procs']} processes x 1 env, {mp_['seconds']:.0f} s "
-                                          f"(oracle/cpu_bench.py --impl py_rules)")
+                                          f"(oracle/cpu_bench.py --impl py_rules, two audits per step)")
     return out
 
 
@@ -157,13 +197,18 @@ def cpu_baseline(proc, tb, max_steps, seconds, obs_dims=None, config="c3"):
     from oracle.cpu_ref import CpuRefEnv
     rng = np.random.default_rng(0)
     env = CpuRefEnv(pool[0], tb, max_steps)
+    q, pending = 0, False
     k, t1 = 0, time.perf_counter()
     while time.perf_counter() - t1 < min(3.0, seconds):
-        _, term, trunc = env.step(int(rng.integers(4)))
-        k += 1
-        if term or trunc:
-            env.p = pool[k % len(pool)]
+        if pending:          # next-step autoreset: one env-step, as the GPU kernel counts it
+            q = (q + 1) % len(pool)
+            env.p = pool[q]
             env.reset()
+            pending = False
+        else:
+            _, term, trunc = env.step(int(rng.integers(4)))
+            pending = term or trunc
+        k += 1
     py_rate = k / (time.perf_counter() - t1)
     out = {"value": round(c_rate, 1), "unit": "env-steps/s", "cores": 1, "kind": "port",
            "sample": f"oracle/sparc_oracle.c, {n} envs x {steps} steps, random actions, next-step autoreset, "
@@ -173,7 +218,7 @@ def cpu_baseline(proc, tb, max_steps, seconds, obs_dims=None, config="c3"):
            "value_1core": round(c_rate, 1),
            "python_port_value": round(py_rate, 1),
            "python_port_sample": "oracle/cpu_ref.py (reference step() restated in pure Python, no rule "
-                                 f"audit), 1 env, {k} steps, 1 thread"}
+                                 f"audit), 1 env, {k} steps incl. next-step autoreset steps, 1 thread"}
     # the same oracle, one process per core (BASELINE.md CPU-baseline plan), in a child process
     # that never touches the GPU; up to 16 cores (one GPU's share of the box)
     cmd = [sys.executable, "-m", "oracle.cpu_bench", "--config", config, "--seconds", str(seconds),
@@ -214,6 +259,30 @@ def _cpu_bench_multi(config, impl, max_steps, seconds):
         return json.loads(r.stdout.strip().splitlines()[-1])
     except (subprocess.SubprocessError, ValueError, IndexError):
         return None
+
+
+def achievable_bw(dev, gib=2, reps=10):
+    """Achievable HBM bandwidth on THIS box, measured in the same run as the bench line (SURVEY
+    §8d): torch's fill_ (pure stores, the c4 plane writer's traffic) and copy_ (read + write) over
+    a `gib` GiB buffer, `reps` launches after two warm-ups, HIP events; GB/s = 1e9 B/s."""
+    import torch
+    n = gib << 30
+    a = torch.empty(n, dtype=torch.uint8, device=dev)
+    b = torch.empty(n, dtype=torch.uint8, device=dev)
+    out = {}
+    for name, fn, moved in (("store", lambda k: a.fill_(k & 0xFF), n), ("copy", lambda k: b.copy_(a), 2 * n)):
+        fn(1)
+        fn(2)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for k in range(reps):
+            fn(k)
+        e1.record()
+        e1.synchronize()
+        out[f"{name}_gbs"] = round(moved * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
+    del a, b
+    torch.cuda.empty_cache()
+    return out
 
 
 def csrc_hash():
@@ -374,10 +443,14 @@ def main():
     if obs:
         ovis = torch.empty((T, n, X, Y), dtype=torch.int32, device=dev)
         oag = torch.empty_like(ovis)
-    g = torch.Generator(device=dev)
-    g.manual_seed(1234 + rank)
     RA, RO = min(max(K, W), 8), min(max(K, W), 2)   # distinct action tiles / output tiles
-    actions = torch.randint(0, 4, (RA, T, n), dtype=torch.uint8, device=dev, generator=g)
+    # action tile j = env.action_space.sample() for every env and step, drawn on the GPU by the
+    # counter-based generator keyed by the GLOBAL env id (sparc_rand_action(ACTION_SEED,
+    # env_offset + i, j * T + t)): the ranks' shards together hold exactly the tiles of one
+    # process over all world * n envs
+    actions = torch.empty((RA, T, n), dtype=torch.uint8, device=dev)
+    for j in range(RA):
+        vec.random_actions(T, seed=ACTION_SEED, t0=j * T, out=actions[j])
     rew = torch.empty((RO, T, n), dtype=torch.int8, device=dev)
     flags = torch.empty((RO, T, n), dtype=torch.uint8, device=dev)
     stats = torch.zeros((n, 4), dtype=torch.int32, device=dev)
@@ -433,6 +506,8 @@ def main():
     elapsed = sdist.max_over_ranks(t1 - t0, dev)
     summary = sdist.summarize(gathered)
 
+    if rank == 0 and args.stats_out:
+        np.save(args.stats_out, gathered.cpu().numpy())
     kern_ms = [a.elapsed_time(b) for (a, b), _ in events]
     steps_per_launch = [c for _, c in events]
     avg_ms = float(np.mean(kern_ms))
@@ -442,14 +517,18 @@ def main():
     # algorithmic HBM bytes per launch: per env-step action 1 + reward 1 + flags 1; per env and
     # launch the state (load + store) and, for rollouts, the stats record (load + store)
     sb = state_bytes_per_env(table.words, tb)
-    per_env_launch = 2 * sb + (32 if args.mode == "rollout" else 0) + (96 if rules else 0)
+    # rule rollouts: k_rollout1r (every puzzle in the region-code table: no exact-fit memo) or the
+    # generic k_rollout<..., RULES> (the per-env memo loaded and stored, 48 B each way)
+    rule_kernel = rule_rollout_kernel(proc, table) if rules else None
+    memo_bytes = 96 if rule_kernel == "k_rollout" else 0
+    per_env_launch = 2 * sb + (32 if args.mode == "rollout" else 0) + memo_bytes
     per_step = 3 + (2 * plane_bytes if obs and args.mode == "rollout" else 0) + (2 if rules else 0)
     bytes_launch = n * (per_step * avg_T + per_env_launch)
     achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
     if args.mode != "rollout":
         kernel = "k_step"
     elif rules:
-        kernel = "k_rollout"     # k_rollout<W, ..., RULES>: the audit after every step
+        kernel = rule_kernel     # the audit after every step
     elif table.words == 1 and not obs:
         # batches of whole 256-env workgroups: the split move / trie kernel
         kernel = "k_rollout1s" if n % 256 == 0 and chunk >= 16 else "k_rollout1"
@@ -472,6 +551,9 @@ def main():
                  "frac": round(valu / (avg_ms * 1e-3) / VALU_PEAK_WAVE_INSTS, 4),
                  "note": "VALU issue roofline: SQ_INSTS_VALU of the committed PMC pass / the live kernel time / "
                          "(1,024 SIMDs x one wave64 VALU per 2 cycles x 2.4 GHz)"}
+    # the HBM-bound configuration (observation planes: ~99 % of its bytes are plane stores) gets
+    # this box's achievable store bandwidth beside the 8 TB/s peak
+    ach = achievable_bw(dev) if obs and args.mode == "rollout" else None
     backend = dist.get_backend() if dist.is_initialized() else None
     observed_world = dist.get_world_size() if dist.is_initialized() else 1
     out = {
@@ -495,7 +577,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8/u64 (integer bitboards)",
-        "data": "synthetic SPaRC-schema puzzles (sparc_gym_amd.synthetic, seed 0); uniform random actions in HBM",
+        "data": "synthetic SPaRC-schema puzzles (sparc_gym_amd.synthetic, seed 0); uniform random actions in HBM "
+                "(sparc_rand_action of the global env id, drawn before the timed region)",
         "config": {"workload": f"{args.config}: {n} envs/GPU, lattices {['%dx%d' % (2*w+1, 2*h+1) for w, h in sizes]}, "
                                f"{'full property set' if full else 'base planes'}, traceback={tb}, "
                                f"max_steps={args.max_steps}, next-step autoreset, {args.puzzles} puzzles"
@@ -513,6 +596,9 @@ def main():
                      "traffic_source": (f"profiles/pmc_traffic.json [{workload}][{kernel}], csrc {csrc_hash()}"
                                         if pmc else f"none recorded for csrc {csrc_hash()}"),
                      "issue": issue,
+                     **({"achievable_gbs": ach["store_gbs"], "frac_of_achievable": round(achieved / ach["store_gbs"], 4),
+                         "achievable": dict(ach, source="torch fill_ (stores) / copy_ (read + write) over 2 GiB, 10 "
+                                                        "launches, this box, this run")} if ach else {}),
                      "kernel": kernel, "kernel_avg_ms": round(avg_ms, 4), "launches": len(kern_ms),
                      "algorithmic_bytes_per_launch": int(bytes_launch),
                      "bytes_model": f"per env-step {per_step} B (action, reward code, flags"
@@ -521,7 +607,7 @@ def main():
                                     f"); per env per launch "
                                     f"{per_env_launch} B (state {sb} B load+store"
                                     f"{', stats 16 B load+store' if args.mode == 'rollout' else ''}"
-                                    f"{', exact-fit memo 48 B load+store' if rules else ''})"},
+                                    f"{', exact-fit memo 48 B load+store' if memo_bytes else ''})"},
         "episodes": summary,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and rules:

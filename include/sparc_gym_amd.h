@@ -147,6 +147,12 @@ int sparc_step_host(void *ctx, const uint8_t *actions, int8_t *reward, uint8_t *
 int sparc_rollout_device(void *ctx, int32_t T, const uint8_t *d_actions, uint64_t seed, uint64_t t0,
                          int8_t *d_reward, uint8_t *d_flags, int32_t *d_stats);
 
+/* env.action_space.sample() (Final_Product.py:29) for every env and T steps, into HBM:
+ * d_actions [T][N] uint8, entry (t, i) = sparc_rand_action(seed, env_offset+i, t0+t) — the
+ * actions a NULL-action rollout draws, seeded by the GLOBAL env id so that the shards of a
+ * multi-GPU job hold exactly the actions of one process over all envs.  Asynchronous. */
+int sparc_random_actions_device(void *ctx, int32_t T, uint64_t seed, uint64_t t0, uint8_t *d_actions);
+
 /* obs['base']['visited'] / obs['base']['agent_location'] as dense int32 planes
  * [N][x_dim][y_dim] (x_dim >= max x_size, y_dim >= max y_size; device pointers, either may be
  * NULL).  The reference returns these planes by reference every step (SPaRC_Gym.py:979). */
@@ -254,9 +260,11 @@ enum {
     SPARC_RULE_TRIANGLES = 1 << 6,            /* 622-646                             */
     SPARC_RULE_POLY_YLOP = 1 << 7,            /* 648-838                             */
     SPARC_RULE_ALL = 1 << 8,                  /* all_rules_satisfied 931-936         */
-    /* not a rule: an exact-fit search of this env (_polyfit_region_exact, 738-853) passed 2^26
-     * nodes without an answer; its poly/ylop bit (and ALL) then read 0, and the host refuses to
-     * build that env's rule_status.  The reference has no cap; no pool of this repo reaches it. */
+    /* not a rule: an exact-fit search of this audit (_polyfit_region_exact, 738-853) passed the
+     * GPU's node cap (sparc_set_rule_limits; 2^26 by default) and is PENDING: its region counts
+     * as passing until sparc_rules_finish has run the search to its end on the host (the
+     * reference's search is unbounded) and patched POLY_YLOP / ALL.  Never set after
+     * sparc_rules_finish (sparc_rules_host calls it itself). */
     SPARC_RULE_SEARCH_EXHAUSTED = 1 << 9
 };
 
@@ -268,6 +276,20 @@ int sparc_load_rules(void *ctx, const sparc_rules_table *table);
  * check and the exact fit).  Device pointers; any output may be NULL. */
 int sparc_rules_device(void *ctx, uint16_t *d_bits, uint8_t *d_region, uint64_t *d_fit);
 int sparc_rules_host(void *ctx, uint16_t *bits, uint8_t *region, uint64_t *fit);
+
+/* Finish the exact-fit searches that passed the GPU's node cap in the LAST audit call
+ * (sparc_rules_device, or sparc_rollout_rules_device: its d_rule_bits) on the host, without a
+ * cap, and patch that call's outputs: SPARC_RULE_SEARCH_EXHAUSTED cleared, POLY_YLOP and ALL
+ * cleared when a region does not fit, and (d_fit, may be NULL) the fit bits of the regions that
+ * do.  Call it after each such call, before reading its bits (a no-op sync when nothing passed
+ * the cap).  Synchronous.  SPARC_E_STATE when more than 65,536 searches of one call passed it. */
+int sparc_rules_finish(void *ctx, uint16_t *d_bits, uint64_t *d_fit);
+
+/* Limits of the rule audit: fit_cap_nodes = search nodes one exact fit runs on the GPU before the
+ * host finishes it (0: 2^26); table_entries = the region-code table budget in 4-bit entries
+ * (0: 2^28 = 128 MB; puzzles past it are audited by the memoised search instead).  The cap applies
+ * to the following audits and the next sparc_load_rules, the budget to the next sparc_load_rules. */
+int sparc_set_rule_limits(void *ctx, uint32_t fit_cap_nodes, uint64_t table_entries);
 
 /* ---- multi-GPU: the end-of-batch gather over RCCL (xGMI) -------------------------------------
  * The envs shard across GPUs as contiguous global id ranges (env_offset), one process and one

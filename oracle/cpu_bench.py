@@ -13,7 +13,8 @@ one JSON line: {"value": env-steps/s summed over processes, "procs": P, ...}.
 
 --impl py runs the pure-Python restatement instead (oracle/cpu_ref.py: the reference's step()
 core at reference speed, one env at a time), --impl py_rules the same plus the rule audit of
-oracle/rules_ref.py once per step (the reference's full step(): _validate_rules, 941-950).
+oracle/rules_ref.py twice per step, as the reference's full step() runs _validate_rules (941-950) at
+1227 and again in _get_info (1011).  Autoreset steps count as env-steps, as on the GPU.
 """
 from __future__ import annotations
 
@@ -76,7 +77,10 @@ def _worker(args):
 
 
 def _worker_py(args):
-    """One env at a time through oracle/cpu_ref.py (+ oracle/rules_ref.py's audit per step)."""
+    """One env at a time through oracle/cpu_ref.py (+ oracle/rules_ref.py's audit twice per step,
+    SPaRC_Gym.py:1227 and 1011).  Next-step autoreset counted as the GPU kernel and the C oracle
+    count it: the step after a done step is the reset (reset() audits twice too: 182, 1011), one
+    env-step."""
     proc, tb, max_steps, seconds, rules, rank = args
     from oracle.cpu_ref import CpuRefEnv
     from oracle import rules_ref
@@ -86,16 +90,21 @@ def _worker_py(args):
     rng = np.random.default_rng(rank)
     q = (rank * 2654435761) % len(pool)
     env = CpuRefEnv(pool[q], tb, max_steps)
+    pending = False
     k, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
-        _, term, trunc = env.step(int(rng.integers(4)))
-        if rules:
-            rules_ref.audit(proc[q], env.path, env.loc, term, trunc)
-        k += 1
-        if term or trunc:
+        if pending:
             q = (q + 1) % len(pool)
             env.p = pool[q]
             env.reset()
+            term = trunc = pending = False
+        else:
+            _, term, trunc = env.step(int(rng.integers(4)))
+            pending = term or trunc
+        if rules:
+            rules_ref.audit(proc[q], env.path, env.loc, term, trunc)
+            rules_ref.audit(proc[q], env.path, env.loc, False, False)
+        k += 1
     return k, time.perf_counter() - t0
 
 

@@ -10,7 +10,6 @@
 //   k_rules    rule audit of the current state                      (_validate_rules, 941-950)
 // No MFMA: this is integer / bitboard work, bound by latency and HBM.
 #include <hip/hip_runtime.h>
-#include <rccl/rccl.h>
 #include <dlfcn.h>
 
 #include <algorithm>
@@ -40,9 +39,10 @@ constexpr int kWaves = kBlock / 64;
 // per wave
 template <int W, int EPW>
 __host__ __device__ constexpr size_t tiles_lds_bytes() { return (size_t)kWaves * 3 * EPW * kTile; }
-// per-wave LDS tile of the rule bits of a rule rollout ([16 steps][EPW envs] uint16)
+// per-wave LDS tile of the rule bits of a rule rollout ([16 steps][EPW envs] uint16), then one
+// flag word per wave (the audit-pair join, k_rollout)
 template <int EPW>
-__host__ __device__ constexpr size_t bits_lds_bytes() { return (size_t)kWaves * 2 * EPW * kTile; }
+__host__ __device__ constexpr size_t bits_lds_bytes() { return (size_t)kWaves * 2 * EPW * kTile + 4 * kWaves; }
 constexpr size_t kMaxDynLds = 160 * 1024;   // one workgroup may own all 160 KiB (gfx950)
 
 // LDS bytes of the staged puzzle rows: (W = 1) compact row + reset board, or (W > 1) info +
@@ -74,6 +74,29 @@ __global__ void __launch_bounds__(kBlock) k_reset(Params p, const uint32_t* __re
     e.reset(p, src, pid);
     e.store(p, src, i);
     if (flg) flg[i] = (uint8_t)(e.legal << 2);
+}
+
+// counter-based random actions [T][N]: entry (t, i) = sparc_rand_action(seed, env_offset + i,
+// t0 + t), the device form of env.action_space.sample() (Final_Product.py:29) for every env.
+// Seeded by the GLOBAL env id, so the shards of a multi-GPU job draw exactly the actions one
+// process over all envs would (the RAND rollouts draw the same values in registers).  Four
+// envs per lane, one 4-byte store when the row is aligned.
+__global__ void __launch_bounds__(kBlock) k_rand_actions(uint64_t seed, uint64_t env_offset, uint64_t t0, uint32_t n,
+                                                         uint32_t T, uint8_t* __restrict__ out) {
+    const uint32_t per_row = (n + 3u) / 4u;
+    const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= (uint64_t)per_row * T) return;
+    const uint32_t t = (uint32_t)(k / per_row), i0 = (uint32_t)(k - (uint64_t)t * per_row) * 4u;
+    uint8_t* row = out + (size_t)t * n;
+    uint32_t v = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j)
+        if (i0 + j < n) v |= uint_rand_action(seed, env_offset + i0 + j, t0 + t) << (8u * j);
+    if (i0 + 4u <= n && ((reinterpret_cast<uintptr_t>(row + i0) & 3u) == 0)) {
+        *reinterpret_cast<uint32_t*>(row + i0) = v;
+    } else {
+        for (uint32_t j = 0; j < 4 && i0 + j < n; ++j) row[i0 + j] = (uint8_t)(v >> (8u * j));
+    }
 }
 
 template <int W, bool TB>
@@ -308,6 +331,13 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
     constexpr size_t kBitsOff = kObsOff + (OBS ? obs_lds_bytes<W>() : 0);
     constexpr size_t kTableOff = kBitsOff + (RULES ? bits_lds_bytes<EPW>() : 0);
     uint16_t* tbits = reinterpret_cast<uint16_t*>(smem + kBitsOff) + wv * (EPW * kTile);
+    // RULES: per wave pair, set by the partner wave when it is done; the lead wave stores the
+    // state and memo only after that, so the partner never loads a state the lead already wrote
+    uint32_t* pair_done = reinterpret_cast<uint32_t*>(smem + kBitsOff + (size_t)kWaves * 2 * EPW * kTile);
+    if constexpr (RULES) {
+        if (threadIdx.x < kWaves) pair_done[threadIdx.x] = 0u;
+        __syncthreads();
+    }
     PuzzleSrc<W> src{p.tab.info, p.tab.root, p.tab.open, p.tab.init, p.tab.row1};
     ObsWave<W>* ow = reinterpret_cast<ObsWave<W>*>(smem + kObsOff) + wv;
     const uint16_t* lut = reinterpret_cast<const uint16_t*>(smem + kObsOff + kWaves * sizeof(ObsWave<W>));
@@ -389,12 +419,13 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
             for (int k = 0; k < W; ++k) vb.w[k] = v[k];
             const uint32_t xy = e.agent_xy(p);
             RuleOut<W> ro;
+            const uint64_t pos = (uint64_t)t * n + i;   // this audit's rule-bits entry (FitQueue)
             if constexpr (W == 1) {   // the puzzle's rule data stays in registers until the env's puzzle changes
                 if (e.pid != pr.q) pr = puzzle_rules<W>(p, rtr.rt, e.pid);
-                ro = audit<W>(p, rtr.rt, pr, vb, xy & 0xFFu, (xy >> 8) & 0xFFu, nullptr, &memo);
+                ro = audit<W>(p, rtr.rt, pr, vb, xy & 0xFFu, (xy >> 8) & 0xFFu, nullptr, &memo, pos);
             } else {
                 ro = audit<W>(p, rtr.rt, puzzle_rules<W>(p, rtr.rt, e.pid), vb, xy & 0xFFu, (xy >> 8) & 0xFFu, nullptr,
-                              &memo);
+                              &memo, pos);
             }
             *slot = (uint16_t)ro.bits;
         }
@@ -475,6 +506,18 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
                 }
                 obs(t);
             }
+        }
+    }
+    if constexpr (RULES) {   // the join of the audit pair (see pair_done)
+        const uint32_t pair = wv / kAuditWaves;
+        if (!lead) {
+            __hip_atomic_store(&pair_done[pair], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
+            // bounded: the partner runs the same loop and always gets here
+            for (uint32_t k = 0; k < (1u << 24) &&
+                                 __hip_atomic_load(&pair_done[pair], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u;
+                 ++k)
+                __builtin_amdgcn_s_sleep(2);
         }
     }
     if (!active || !lead) return;
@@ -891,6 +934,212 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
 }
 
 // ---------------------------------------------------------------------------------------------
+// W = 1 rollout with the rule audit after every step (k_rollout1r: sparc_rollout_rules_device on
+// pools whose every puzzle has a region-code table).  The reference audits every step()
+// (_validate_rules at SPaRC_Gym.py:1227, again in _get_info 1011; info['rule_status'] 941-950).
+// That audit — a flood fill per region and one table lookup per region (sparc_rules.hpp) — costs
+// about ten times the step and is one latency-bound dependency chain per lane, so it runs in
+// waves of its own: per 64 envs one STEP wave (Env<1>::advance: the step, the stats, the outputs)
+// and A AUDIT waves, audit wave q auditing the steps t with t % A == q.  Nothing is
+// computed twice and no audit wave carries step state.
+//   The step wave hands every env-step over as ONE u64 in an LDS ring: the visited board (the
+// bits below kRingShift: every W = 1 pool with x_size * pitch <= 57) | the agent's bit << 57 |
+// autoreset << 63.  The audit wave follows the puzzle index through the autoresets itself (a
+// reset loads (index + 1) % P, 1087) and keeps the puzzle's rule planes in registers while it
+// stays on a puzzle.
+//   Per workgroup 64 * G envs = G step waves (0..G-1) + G * A audit waves (group g = wave % G);
+// tiles of RT steps, one barrier per tile.  In interval k the step waves step tile k and store
+// the rewards / flags of tile k-1 and the rule bits of tile k-2 (whole 16-B pieces of the
+// workgroup's rows), the audit waves audit tile k-1.  The
+// state is only read before B_0 and written after the last barrier, so the audit waves' initial
+// puzzle index is never a later one.
+// Shape <G, A, RT>: G 64-env groups per workgroup, A audit waves per group (so G * (1 + A) waves
+// <= 16), RT steps per tile (a multiple of A).
+template <int G, int A, int RT>
+struct R1Geom {
+    static_assert(G * (1 + A) <= 16 && RT % A == 0, "k_rollout1r shape");
+    static constexpr int kBlock = 64 * G * (1 + A);
+    static constexpr uint32_t kEnvs = 64u * G;                            // envs per workgroup (a tile row)
+    static constexpr size_t kRing = 0;                                      // [2][RT][kEnvs] u64
+    static constexpr size_t kRew = kRing + 2 * RT * kEnvs * 8;             // [2][RT][kEnvs] reward codes
+    static constexpr size_t kFlg = kRew + 2 * RT * kEnvs;                  // [2][RT][kEnvs] flags
+    static constexpr size_t kBits = kFlg + 2 * RT * kEnvs;                 // [2][RT][kEnvs] u16 rule bits
+    static constexpr size_t kAct = kBits + 2 * RT * kEnvs * 2;             // [G][RT][64] actions of the tile
+    static constexpr size_t kStk = kAct + G * RT * 64;                     // [G][64 moves][64] move stacks
+    static constexpr size_t kBase = kStk + (size_t)G * 64 * 64;            // then the W = 1 puzzle rows
+};
+constexpr uint32_t kRingShift = 57;
+
+template <bool TB, bool RAND, bool LDS_TABLE, int G, int A, int RT>
+__global__ void __launch_bounds__(64 * G * (1 + A))
+    k_rollout1r(Params p, int32_t T, const uint8_t* __restrict__ act, uint64_t seed, uint64_t t0,
+                int8_t* __restrict__ rew, uint8_t* __restrict__ flg, int4* __restrict__ stats, uint32_t tiled,
+                RulesTab rt, uint16_t* __restrict__ bits) {
+    using Geo = R1Geom<G, A, RT>;
+    constexpr uint32_t E = Geo::kEnvs;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t g = wv % (uint32_t)G;                         // the wave's 64-env group
+    const size_t n = p.n;
+    const uint32_t wg_base = blockIdx.x * E;
+    const uint32_t col = g * 64u + lane;                         // the env's column in a tile row
+    const uint32_t i = wg_base + col;
+    const bool active = i < n;
+    const bool full = tiled && (size_t)wg_base + E <= n;         // block-uniform: 16-B row pieces
+    const int32_t K = (T + RT - 1) / RT;
+    uint64_t* ring = reinterpret_cast<uint64_t*>(smem + Geo::kRing);
+    uint8_t* trw = smem + Geo::kRew;
+    uint8_t* tfl = smem + Geo::kFlg;
+    uint16_t* tbt = reinterpret_cast<uint16_t*>(smem + Geo::kBits);
+    auto at = [](uint32_t b, int32_t j, uint32_t c) { return (b * (uint32_t)RT + (uint32_t)j) * E + c; };
+    auto tile_cnt = [&](int32_t k) { return T - k * RT < RT ? T - k * RT : RT; };
+    PuzzleSrc<1> src{p.tab.info, p.tab.root, p.tab.open, p.tab.init, p.tab.row1};
+    if constexpr (LDS_TABLE) {
+        const uint32_t P = p.tab.num_puzzles;
+        uint4* lrow1 = reinterpret_cast<uint4*>(smem + Geo::kBase);
+        uint64_t* linit = reinterpret_cast<uint64_t*>(lrow1 + P);
+        for (uint32_t k = threadIdx.x; k < P; k += Geo::kBlock) {
+            lrow1[k] = p.tab.row1[k];
+            linit[k] = p.tab.init[k];
+        }
+        __syncthreads();
+        src = PuzzleSrc<1>{p.tab.info, p.tab.root, p.tab.open, linit, lrow1};
+    }
+
+    if (wv < (uint32_t)G) {                                      // ---- step waves
+        using Stack = typename std::conditional<TB, LdsStack<64>, RegStack>::type;
+        Env<1, TB, Stack> e;
+        if constexpr (TB) e.stk.col = smem + Geo::kStk + g * 4096u + lane;
+        if (active) e.load(p, src, i);
+        int4 acc = make_int4(0, 0, 0, 0);
+        const uint64_t gid = p.env_offset + i;
+        uint8_t* ta = smem + Geo::kAct + g * (RT * 64u);
+        const uint32_t r = lane >> 2, c = (lane & 3u) * 16u;    // this lane's 16-B piece of an action tile
+        const bool tact = !RAND && full;                         // actions through the tile prefetch
+        u32x4 anext = {0u, 0u, 0u, 0u};
+        if (tact && (int32_t)r < tile_cnt(0)) anext = nt_load16(act + (size_t)r * n + wg_base + g * 64u + c);
+        // tile kt's rewards / flags, or rule bits, from LDS to HBM by the E step-wave lanes
+        auto store_rf = [&](int32_t kt) {
+            const int32_t cnt = tile_cnt(kt);
+            const uint32_t b = (uint32_t)kt & 1u;
+            if (full) {
+                constexpr uint32_t kPer = E / 16u;               // 16-B pieces per row
+                for (uint32_t pi = col; pi < kPer * (uint32_t)cnt; pi += E) {
+                    const uint32_t row = pi / kPer, cb = (pi % kPer) * 16u;
+                    const size_t o = (size_t)(kt * RT + (int32_t)row) * n + wg_base + cb;
+                    if (rew) nt_store16(reinterpret_cast<uint8_t*>(rew) + o, *reinterpret_cast<const u32x4*>(trw + at(b, (int32_t)row, cb)));
+                    if (flg) nt_store16(flg + o, *reinterpret_cast<const u32x4*>(tfl + at(b, (int32_t)row, cb)));
+                }
+            } else if (active) {
+                for (int32_t j = 0; j < cnt; ++j) {
+                    const size_t o = (size_t)(kt * RT + j) * n + i;
+                    if (rew) rew[o] = (int8_t)trw[at(b, j, col)];
+                    if (flg) flg[o] = tfl[at(b, j, col)];
+                }
+            }
+        };
+        auto store_bits = [&](int32_t kt) {
+            const int32_t cnt = tile_cnt(kt);
+            const uint32_t b = (uint32_t)kt & 1u;
+            if (full) {
+                constexpr uint32_t kPer = E / 8u;                // 16-B pieces (8 entries) per row
+                for (uint32_t pi = col; pi < kPer * (uint32_t)cnt; pi += E) {
+                    const uint32_t row = pi / kPer, ce = (pi % kPer) * 8u;
+                    const size_t o = (size_t)(kt * RT + (int32_t)row) * n + wg_base + ce;
+                    nt_store16(reinterpret_cast<uint8_t*>(bits + o), *reinterpret_cast<const u32x4*>(tbt + at(b, (int32_t)row, ce)));
+                }
+            } else if (active) {
+                for (int32_t j = 0; j < cnt; ++j) bits[(size_t)(kt * RT + j) * n + i] = tbt[at(b, j, col)];
+            }
+        };
+        __syncthreads();                                         // B_0
+        for (int32_t k = 0; k < K; ++k) {
+            const int32_t cnt = tile_cnt(k);
+            const uint32_t b = (uint32_t)k & 1u;
+            if (tact) {
+                const u32x4 acur = anext;
+                if (k + 1 < K && (int32_t)r < tile_cnt(k + 1))
+                    anext = nt_load16(act + (size_t)((k + 1) * RT + (int32_t)r) * n + wg_base + g * 64u + c);
+                if ((int32_t)r < cnt) *reinterpret_cast<u32x4*>(ta + r * 64u + c) = acur;
+                wave_lds_fence();
+            }
+#pragma unroll 1
+            for (int32_t j = 0; j < cnt; ++j) {
+                const int32_t t = k * RT + j;
+                uint32_t a = 0;
+                if constexpr (RAND) a = uint_rand_action(seed, gid, t0 + (uint64_t)t);
+                else if (tact) a = ta[j * 64 + (int32_t)lane];
+                else if (active) a = act[(size_t)t * n + i];
+                uint32_t f = 0;
+                int code = 0;
+                uint64_t w = 0;
+                if (active) {
+                    code = e.advance(p, src, a, f);
+                    acc.x += code;
+                    acc.y += (int)e.pending;
+                    acc.z += (int)e.solved;
+                    acc.w += (int)e.was_reset;
+                    uint64_t v[1];
+                    uint32_t ab;
+                    e.obs_words(p, src, v, ab);
+                    w = v[0] | ((uint64_t)(ab | (((f >> 6) & 1u) << 6)) << kRingShift);
+                }
+                ring[at(b, j, col)] = w;
+                trw[at(b, j, col)] = (uint8_t)code;
+                tfl[at(b, j, col)] = (uint8_t)f;
+            }
+            if (k >= 1) store_rf(k - 1);
+            if (k >= 2) store_bits(k - 2);
+            __syncthreads();                                     // B_{k+1}
+        }
+        store_rf(K - 1);                                         // interval K: the last tile's audits run
+        if (K >= 2) store_bits(K - 2);
+        __syncthreads();                                         // B_{K+1}
+        store_bits(K - 1);
+        if (!active) return;
+        e.store(p, src, i);
+        if (stats) {
+            int4 st = stats[i];
+            st.x += acc.x;
+            st.y += acc.y;
+            st.z += acc.z;
+            st.w += acc.w;
+            stats[i] = st;
+        }
+        return;
+    }
+
+    // ---- audit waves
+    const uint32_t q = wv / (uint32_t)G - 1u;                    // audits the steps t % A == q
+    const uint32_t NP = p.tab.num_puzzles;
+    uint32_t pid = active ? p.st.pid[i] : 0u;
+    PuzzleRules<1> pr;
+    pr.q = 0xFFFFFFFFu;
+    __syncthreads();                                             // B_0
+    __syncthreads();                                             // B_1 (interval 0: no tile yet)
+    for (int32_t k = 1; k <= K; ++k) {
+        const int32_t kt = k - 1, cnt = tile_cnt(kt);
+        const uint32_t b = (uint32_t)kt & 1u;
+#pragma unroll 1
+        for (int32_t j = 0; j < cnt; ++j) {
+            const uint64_t w = ring[at(b, j, col)];
+            if (w >> 63) pid = pid + 1u == NP ? 0u : pid + 1u;   // an autoreset step: reset(), 1087
+            if ((uint32_t)j % (uint32_t)A != q) continue;        // another audit wave's step
+            uint32_t out = 0;
+            if (active) {
+                if (pid != pr.q) pr = puzzle_rules<1>(p, rt, pid);
+                BB<1> vb;
+                vb.w[0] = w & ((1ull << kRingShift) - 1ull);
+                const uint32_t ab = (uint32_t)(w >> kRingShift) & 63u;
+                out = audit_r<1, NoMemo, true>(p, rt, pr, vb, ab == pr.tbit, nullptr, nullptr).bits;
+            }
+            tbt[at(b, j, col)] = (uint16_t)out;
+        }
+        __syncthreads();                                         // B_{k+1}
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Multi-word split rollout (k_rolloutWs, W = 2 / 4: lattices of 9x9 to 15x15 points).  The same
 // wave roles and tile schedule as k_rollout1s: per workgroup 256 envs = 4 move waves
 // (MoveLaneW, sparc_movew.hpp: the free board in LDS) + 4 trie waves (TrieLane, the same as
@@ -1077,20 +1326,27 @@ __global__ void __launch_bounds__(kBlock) k_rules(Params p, RulesTab rt, uint16_
     // the env's exact-fit memo: the reference audits every step() (SPaRC_Gym.py:1227), and
     // consecutive states share most regions
     FitMemo<kMemo> memo = memos[i];
-    const RuleOut<W> r = audit<W>(p, rt, puzzle_rules<W>(p, rt, q), vis, ps & 0xFFu, (ps >> 8) & 0xFFu, ro, &memo);
+    const RuleOut<W> r = audit<W>(p, rt, puzzle_rules<W>(p, rt, q), vis, ps & 0xFFu, (ps >> 8) & 0xFFu, ro, &memo, i);
     memos[i] = memo;
     if (bits) bits[i] = (uint16_t)r.bits;
     if (fit) fit[i] = r.fit_ok;
 }
 
 // the region-code table (sparc_rules.hpp region_table_word): one word per (puzzle, mask group)
+// (exhausted: the number of codes whose exact-fit search passed the node cap, which the host then
+// finishes, sparc_load_rules)
 template <int W>
 __global__ void __launch_bounds__(kBlock) k_region_table(Params p, RulesTab rt, const uint2* __restrict__ items,
-                                                         uint32_t count, uint32_t* __restrict__ tab) {
+                                                         uint32_t count, uint32_t* __restrict__ tab,
+                                                         uint32_t* __restrict__ exhausted) {
     const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
     if (k >= count) return;
     const uint2 it = items[k];
-    tab[rt.reg_off[it.x] / 8u + it.y] = region_table_word<W>(p, rt, it.x, it.y);
+    const uint32_t w = region_table_word<W>(p, rt, it.x, it.y);
+    tab[rt.reg_off[it.x] / 8u + it.y] = w;
+    uint32_t ex = 0;
+    for (uint32_t j = 0; j < 8; ++j) ex += ((w >> (4u * j + kRcPolyShift)) & 3u) == 3u ? 1u : 0u;
+    if (ex) atomicAdd(exhausted, ex);
 }
 
 // ------------------------------------------------------------------------------ host side
@@ -1132,6 +1388,18 @@ struct Ctx {
     int8_t* r_shape_off = nullptr;
     FitMemo<kMemo>* r_memo = nullptr;   // [N] per-env exact-fit memo of the audit (zeroed at sparc_load_rules)
     uint32_t *r_reg_off = nullptr, *r_reg_tab = nullptr;   // region-code table (sparc_rules.hpp)
+    bool r_tab_all = false;   // every puzzle has a region-code table (k_rollout1r's audit)
+    bool ring_ok = false;     // W = 1 and every board fits below kRingShift (k_rollout1r's ring word)
+    bool rules_generic = false;   // SPARC_RULE_ROLLOUT=generic: rule rollouts on k_rollout<..., RULES> (A/B, tests)
+    int r1r_shape = 0;            // SPARC_R1R_SHAPE: k_rollout1r's <G, A, RT> (0: <4, 3, 12>; A/B, tests)
+    // exact-fit searches past the GPU's node cap (sparc_set_fit_cap) are finished on the host
+    // from these copies of the rule table (sparc_rules.hpp exact_fit, the same code)
+    uint32_t fit_cap = kFitCap;
+    size_t reg_entries = (size_t)1 << 28;   // region-code table budget (entries of 4 bits)
+    std::vector<uint32_t> h_inst, h_inst_range, h_shape_range;
+    std::vector<int8_t> h_shape_off;
+    uint32_t* fq_count = nullptr;   // FitQueue of the audits (sparc_rules_finish)
+    FitTodo* fq_items = nullptr;
     uint16_t* s_bits = nullptr;
     uint8_t* s_region = nullptr;
     uint64_t* s_fit = nullptr;
@@ -1243,6 +1511,53 @@ int launch_check(Ctx* c) {
     return SPARC_OK;
 }
 
+template <int G_, int A_, int RT_>
+struct R1Shape {
+    static constexpr int G = G_, A = A_, RT = RT_;
+};
+
+constexpr uint32_t kFitQueueCap = 1u << 16;   // exact fits past the node cap per audit call
+
+// the loaded rule table as the kernels take it; queue: push searches past the node cap to the
+// FitQueue (audits), or not (the region-code table build: the host scans the table instead)
+RulesTab rules_tab(const Ctx* c, bool queue) {
+    RulesTab rt{};
+    rt.planes = c->r_planes;
+    rt.inst_range = c->r_inst_range;
+    rt.inst = c->r_inst;
+    rt.shape_range = c->r_shape_range;
+    rt.shape_area = c->r_shape_area;
+    rt.shape_off = c->r_shape_off;
+    rt.num_puzzles = c->num_puzzles;
+    rt.area = c->r_area ? 1u : 0u;
+    rt.fit_cap = c->fit_cap;
+    rt.reg_off = c->r_reg_off;
+    rt.reg_tab = c->r_reg_tab;
+    rt.fq = FitQueue{queue ? c->fq_count : nullptr, c->fq_items, kFitQueueCap};
+    return rt;
+}
+
+// _polyfit_region_exact (SPaRC_Gym.py:738-853) of puzzle q's region with cell mask rm on the
+// HOST, without a node cap (the reference's search is unbounded): exact_fit of sparc_rules.hpp,
+// the code the GPU runs, over the host copies of the rule table.  1 fits, 0 does not.
+template <int W>
+int host_fit_w(const Ctx* c, uint32_t q, uint64_t rm) {
+    const uint32_t w0 = c->h_info[4 * (size_t)q], X = w0 & 0xFFu, Y = (w0 >> 8) & 0xFFu;
+    RulesTab rt{};
+    rt.inst = c->h_inst.data();
+    rt.shape_range = c->h_shape_range.data();
+    rt.shape_off = c->h_shape_off.data();
+    const FitIn fin = fit_in(rt, c->h_inst_range[q], X, Y);
+    const uint32_t P = (uint32_t)c->cfg.pitch;
+    BB<W> Rc = BB<W>::zero();
+    for (uint32_t b = 0; b < fin.CX * fin.CY; ++b)
+        if ((rm >> b) & 1ull) Rc.set((2 * (b / fin.CY) + 1) * P + 2 * (b % fin.CY) + 1);
+    return exact_fit<W, uint64_t>(fin, Rc, rm, ~0ull);
+}
+int host_fit(const Ctx* c, uint32_t q, uint64_t rm) {
+    return c->W == 1 ? host_fit_w<1>(c, q, rm) : c->W == 2 ? host_fit_w<2>(c, q, rm) : host_fit_w<4>(c, q, rm);
+}
+
 }  // namespace
 
 extern "C" {
@@ -1273,6 +1588,8 @@ int sparc_create(int device, const sparc_config* cfg, void** ctx_out) {
     c->device = device;
     c->n = (uint32_t)cfg->num_envs;
     c->W = cfg->words;
+    if (const char* v = getenv("SPARC_RULE_ROLLOUT")) c->rules_generic = strcmp(v, "generic") == 0;
+    if (const char* v = getenv("SPARC_R1R_SHAPE")) c->r1r_shape = atoi(v);
     const size_t n = c->n;
     auto cleanup = [&](int code) {
         sparc_destroy(c);
@@ -1307,7 +1624,7 @@ int sparc_destroy(void* ctx) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->vis, c->dirs, c->pos, c->aux, c->step, c->pid, c->t_open, c->t_info, c->t_root, c->t_trie, c->t_trie1, c->t_init, c->t_row1,
                     c->t_trie8, c->t_trow, c->t_mrow, c->t_mroww, c->t_boardw, c->err, c->s_act, c->s_flags, c->s_mask, c->s_rew, c->s_pidx, c->r_planes, c->r_inst_range,
-                    c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off, c->r_memo, c->s_bits, c->s_region, c->s_fit, c->r_reg_off, c->r_reg_tab};
+                    c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off, c->r_memo, c->s_bits, c->s_region, c->s_fit, c->r_reg_off, c->r_reg_tab, c->fq_count, c->fq_items};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->own) (void)hipStreamDestroy(c->own);
@@ -1611,6 +1928,9 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
             }
         }
     }
+    c->ring_ok = W == 1;
+    for (size_t q = 0; q < P; ++q)
+        if ((t->info[4 * q] & 0xFFu) * pitch > kRingShift) c->ring_ok = false;
     c->num_puzzles = (uint32_t)t->num_puzzles;
     c->num_nodes = (uint32_t)t->num_nodes;
     c->h_info.assign(t->info, t->info + 4 * P);
@@ -1679,6 +1999,21 @@ int sparc_step_host(void* ctx, const uint8_t* act, int8_t* rew, uint8_t* flags) 
     HIPCHK(c, hipMemcpyAsync(rew, c->s_rew, c->n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(flags, c->s_flags, c->n, hipMemcpyDeviceToHost, c->stream));
     return sparc_sync(c);
+}
+
+int sparc_random_actions_device(void* ctx, int32_t T, uint64_t seed, uint64_t t0, uint8_t* d_actions) {
+    DevGuard dg;
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c) return fail(nullptr, SPARC_E_INVALID, "null context");
+    if (!d_actions) return fail(c, SPARC_E_INVALID, "null actions");
+    if (T < 0) return fail(c, SPARC_E_INVALID, "T must be >= 0");
+    if (T == 0) return SPARC_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    const uint64_t lanes = (uint64_t)((c->n + 3u) / 4u) * (uint64_t)T;
+    if (lanes > (uint64_t)kBlock * 0x7FFFFFFFull) return fail(c, SPARC_E_INVALID, "T*N too large");
+    k_rand_actions<<<dim3((unsigned)((lanes + kBlock - 1) / kBlock)), kBlock, 0, c->stream>>>(
+        seed, (uint64_t)c->cfg.env_offset, t0, c->n, (uint32_t)T, d_actions);
+    return launch_check(c);
 }
 
 }  // extern "C"
@@ -1764,6 +2099,44 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
         };
         if (c->cfg.traceback) go1(std::true_type{});
         else go1(std::false_type{});
+        if (lds_rc) return lds_rc;
+        return launch_check(c);
+    }
+    if (rtr && c->W == 1 && c->r_tab_all && c->ring_ok && !c->rules_generic) {
+        // rule rollouts of W = 1 pools with every puzzle in the region-code table: step waves +
+        // audit waves (k_rollout1r; shape <G, A, RT> = c->r1r_shape)
+        auto go_shape = [&](auto geo_c) {
+            using Geo = decltype(geo_c);
+            constexpr int G = Geo::G, A = Geo::A, RT = Geo::RT;
+            using GG = R1Geom<G, A, RT>;
+            const size_t blocks = (c->n + GG::kEnvs - 1) / GG::kEnvs;
+            const size_t tbytes = table_lds_bytes<1>(c->num_puzzles);
+            const bool lds_table = GG::kBase + tbytes <= kMaxDynLds;
+            const size_t shm = GG::kBase + (lds_table ? tbytes : 0);
+            auto launch = [&](auto kern, const uint8_t* a) {
+                if (shm > 64 * 1024 && (lds_rc = allow_big_lds(c, reinterpret_cast<const void*>(kern)))) return;
+                kern<<<dim3((unsigned)blocks), GG::kBlock, shm, c->stream>>>(p, T, a, seed, t0, d_rew, d_flags, st, tiled,
+                                                                            rtr->rt, rtr->bits);
+            };
+            auto go = [&](auto tb) {
+                constexpr bool TB = decltype(tb)::value;
+                if (d_act) {
+                    if (lds_table) launch(k_rollout1r<TB, false, true, G, A, RT>, d_act);
+                    else launch(k_rollout1r<TB, false, false, G, A, RT>, d_act);
+                } else {
+                    if (lds_table) launch(k_rollout1r<TB, true, true, G, A, RT>, nullptr);
+                    else launch(k_rollout1r<TB, true, false, G, A, RT>, nullptr);
+                }
+            };
+            if (c->cfg.traceback) go(std::true_type{});
+            else go(std::false_type{});
+        };
+        switch (c->r1r_shape) {
+            case 1: go_shape(R1Shape<2, 5, 10>{}); break;
+            case 2: go_shape(R1Shape<4, 2, 16>{}); break;
+            case 3: go_shape(R1Shape<2, 4, 12>{}); break;
+            default: go_shape(R1Shape<4, 3, 12>{}); break;
+        }
         if (lds_rc) return lds_rc;
         return launch_check(c);
     }
@@ -1880,9 +2253,7 @@ int sparc_rollout_rules_device(void* ctx, int32_t T, const uint8_t* d_act, uint6
     if (rc) return rc;
     if (!c->rules) return fail(c, SPARC_E_STATE, "sparc_load_rules has not been called");
     if (!d_rule_bits) return fail(c, SPARC_E_INVALID, "null rule_bits");
-    const RuleTrace rtr{RulesTab{c->r_planes, c->r_inst_range, c->r_inst, c->r_shape_range, c->r_shape_area,
-                                 c->r_shape_off, c->num_puzzles, c->r_area ? 1u : 0u, c->r_reg_off, c->r_reg_tab},
-                        d_rule_bits, c->r_memo};
+    const RuleTrace rtr{rules_tab(c, true), d_rule_bits, c->r_memo};
     return rollout_impl(c, T, d_act, seed, t0, d_rew, d_flags, d_stats, nullptr, &rtr);
 }
 
@@ -1998,6 +2369,7 @@ int sparc_load_rules(void* ctx, const sparc_rules_table* t) {
     c->r_shape_range = nullptr; c->r_shape_area = nullptr; c->r_shape_off = nullptr;
     c->r_reg_off = nullptr; c->r_reg_tab = nullptr;
     c->rules = false;
+    c->r_tab_all = false;
     // the device copy: the caller's SPARC_RULE_PLANES planes per puzzle, RP_INST rewritten from the
     // instance list, then the bit-sliced net area of each cell (kAreaPlanes planes, sparc_rules.hpp)
     static_assert(RP_ABI == SPARC_RULE_PLANES, "rule plane layout");
@@ -2039,17 +2411,32 @@ int sparc_load_rules(void* ctx, const sparc_rules_table* t) {
         HIPCHK(c, hipMemcpy(c->r_shape_area, t->shape_area, sizeof(int32_t) * t->num_shapes, hipMemcpyHostToDevice));
     }
     if (t->num_offsets) HIPCHK(c, hipMemcpy(c->r_shape_off, t->shape_off, 2 * (size_t)t->num_offsets, hipMemcpyHostToDevice));
+    // host copies for the exact fits the host finishes (searches past the node cap)
+    c->h_inst.assign(t->inst, t->inst + t->num_inst);
+    c->h_inst.resize(ni, 0u);
+    c->h_inst_range.assign(t->inst_range, t->inst_range + P);
+    c->h_shape_range.assign(t->shape_range, t->shape_range + t->num_shapes);
+    c->h_shape_range.resize(ns, 0u);
+    c->h_shape_off.assign(t->shape_off, t->shape_off + 2 * (size_t)t->num_offsets);
+    c->h_shape_off.resize(2 * no, 0);
+    if (!c->fq_count) {
+        HIPCHK(c, hipMalloc(&c->fq_count, sizeof(uint32_t)));
+        HIPCHK(c, hipMalloc(&c->fq_items, sizeof(FitTodo) * kFitQueueCap));
+    }
+    HIPCHK(c, hipMemset(c->fq_count, 0, sizeof(uint32_t)));
     // the memo's entries name puzzles of the old table: start empty (a zero key matches no region)
     if (!c->r_memo) HIPCHK(c, hipMalloc(&c->r_memo, sizeof(FitMemo<kMemo>) * (size_t)c->n));
     HIPCHK(c, hipMemset(c->r_memo, 0, sizeof(FitMemo<kMemo>) * (size_t)c->n));
     // the per-region check code (squares, stars, poly/ylop area + exact fit) of every region cell
     // mask of each puzzle with at most kRegTabCells cells, computed once here by the audit's own
     // region_code (k_region_table): the audit then looks codes up per region instead of running
-    // the checks (the memo serves the larger puzzles).  At most 128 MB of table.
+    // the checks (the memo serves the larger puzzles, and the puzzles past the table budget:
+    // 2^28 entries, 128 MB, unless sparc_set_rule_limits sets another).  An exact fit that passes
+    // the node cap here is finished on the host, so the table holds only final answers.
     std::vector<uint32_t> reg_off(P, kNoRegTab);
     std::vector<uint2> items;
     size_t entries = 0;
-    constexpr size_t kMaxRegEntries = (size_t)1 << 28;
+    const size_t kMaxRegEntries = c->reg_entries;
     for (size_t q = 0; q < P; ++q) {
         const uint32_t X = info[q].x & 0xFFu, Y = (info[q].x >> 8) & 0xFFu;
         const uint32_t cells = ((X - 1) / 2) * ((Y - 1) / 2);
@@ -2060,6 +2447,7 @@ int sparc_load_rules(void* ctx, const sparc_rules_table* t) {
         for (uint32_t g = 0; g < words; ++g) items.push_back(make_uint2((uint32_t)q, g));
         entries += 8u * words;
     }
+    c->r_tab_all = std::none_of(reg_off.begin(), reg_off.end(), [](uint32_t o) { return o == kNoRegTab; });
     if (!items.empty()) {
         const size_t words = entries / 8;
         uint2* d_items = nullptr;
@@ -2069,16 +2457,34 @@ int sparc_load_rules(void* ctx, const sparc_rules_table* t) {
         HIPCHK(c, hipMemcpy(c->r_reg_off, reg_off.data(), sizeof(uint32_t) * P, hipMemcpyHostToDevice));
         HIPCHK(c, hipMemcpy(d_items, items.data(), sizeof(uint2) * items.size(), hipMemcpyHostToDevice));
         const Params p = make_params(c);
-        const RulesTab rt{c->r_planes, c->r_inst_range, c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off,
-                          c->num_puzzles, c->r_area ? 1u : 0u, c->r_reg_off, nullptr};
+        RulesTab rt = rules_tab(c, false);
+        rt.reg_tab = nullptr;
         const dim3 g((unsigned)((items.size() + kBlock - 1) / kBlock));
-        if (W == 1) k_region_table<1><<<g, kBlock, 0, c->stream>>>(p, rt, d_items, (uint32_t)items.size(), c->r_reg_tab);
-        else if (W == 2) k_region_table<2><<<g, kBlock, 0, c->stream>>>(p, rt, d_items, (uint32_t)items.size(), c->r_reg_tab);
-        else k_region_table<4><<<g, kBlock, 0, c->stream>>>(p, rt, d_items, (uint32_t)items.size(), c->r_reg_tab);
+        const uint32_t n_items = (uint32_t)items.size();
+        if (W == 1) k_region_table<1><<<g, kBlock, 0, c->stream>>>(p, rt, d_items, n_items, c->r_reg_tab, c->fq_count);
+        else if (W == 2) k_region_table<2><<<g, kBlock, 0, c->stream>>>(p, rt, d_items, n_items, c->r_reg_tab, c->fq_count);
+        else k_region_table<4><<<g, kBlock, 0, c->stream>>>(p, rt, d_items, n_items, c->r_reg_tab, c->fq_count);
         rc = launch_check(c);
         HIPCHK(c, hipStreamSynchronize(c->stream));
         HIPCHK(c, hipFree(d_items));
         if (rc) return rc;
+        uint32_t exhausted = 0;
+        HIPCHK(c, hipMemcpy(&exhausted, c->fq_count, sizeof(uint32_t), hipMemcpyDeviceToHost));
+        if (exhausted) {   // finish those searches on the host and rewrite their codes
+            HIPCHK(c, hipMemset(c->fq_count, 0, sizeof(uint32_t)));
+            std::vector<uint32_t> tab(words);
+            HIPCHK(c, hipMemcpy(tab.data(), c->r_reg_tab, sizeof(uint32_t) * words, hipMemcpyDeviceToHost));
+            for (const uint2& it : items) {
+                uint32_t& w = tab[reg_off[it.x] / 8u + it.y];
+                for (uint32_t j = 0; j < 8; ++j) {
+                    const uint32_t sh = 4u * j + kRcPolyShift;
+                    if (((w >> sh) & 3u) != 3u) continue;
+                    const uint32_t poly = host_fit(c, it.x, 8ull * it.y + j) ? 1u : 2u;
+                    w = (w & ~(3u << sh)) | (poly << sh);
+                }
+            }
+            HIPCHK(c, hipMemcpy(c->r_reg_tab, tab.data(), sizeof(uint32_t) * words, hipMemcpyHostToDevice));
+        }
     }
     c->rules = true;
     return SPARC_OK;
@@ -2091,13 +2497,68 @@ int sparc_rules_device(void* ctx, uint16_t* d_bits, uint8_t* d_region, uint64_t*
     if (rc) return rc;
     if (!c->rules) return fail(c, SPARC_E_STATE, "sparc_load_rules has not been called");
     const Params p = make_params(c);
-    const RulesTab rt{c->r_planes, c->r_inst_range, c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off,
-                      c->num_puzzles, c->r_area ? 1u : 0u, c->r_reg_off, c->r_reg_tab};
+    const RulesTab rt = rules_tab(c, true);
     const dim3 g = grid_for(c->n);
     if (c->W == 1) k_rules<1><<<g, kBlock, 0, c->stream>>>(p, rt, d_bits, d_region, d_fit, c->r_memo);
     else if (c->W == 2) k_rules<2><<<g, kBlock, 0, c->stream>>>(p, rt, d_bits, d_region, d_fit, c->r_memo);
     else k_rules<4><<<g, kBlock, 0, c->stream>>>(p, rt, d_bits, d_region, d_fit, c->r_memo);
     return launch_check(c);
+}
+
+int sparc_set_rule_limits(void* ctx, uint32_t fit_cap_nodes, uint64_t table_entries) {
+    DevGuard dg;
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c) return fail(nullptr, SPARC_E_INVALID, "null context");
+    c->fit_cap = fit_cap_nodes ? fit_cap_nodes : kFitCap;
+    c->reg_entries = table_entries ? (size_t)std::min<uint64_t>(table_entries, (uint64_t)1 << 28) : (size_t)1 << 28;
+    return SPARC_OK;
+}
+
+int sparc_rules_finish(void* ctx, uint16_t* d_bits, uint64_t* d_fit) {
+    DevGuard dg;
+    Ctx* c = static_cast<Ctx*>(ctx);
+    int rc = check_ctx(c, false);
+    if (rc) return rc;
+    if (!c->rules) return fail(c, SPARC_E_STATE, "sparc_load_rules has not been called");
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    uint32_t cnt = 0;
+    HIPCHK(c, hipMemcpy(&cnt, c->fq_count, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (cnt == 0) return SPARC_OK;
+    HIPCHK(c, hipMemset(c->fq_count, 0, sizeof(uint32_t)));
+    if (cnt > kFitQueueCap) {
+        char m[200];
+        snprintf(m, sizeof m, "%u exact-fit searches passed the node cap in one audit call (at most %u are finished on "
+                 "the host): raise the cap with sparc_set_rule_limits", cnt, kFitQueueCap);
+        return fail(c, SPARC_E_STATE, m);
+    }
+    if (!d_bits) return fail(c, SPARC_E_INVALID, "null rule bits: the audit's pending exact fits need them");
+    std::vector<FitTodo> todo(cnt);
+    HIPCHK(c, hipMemcpy(todo.data(), c->fq_items, sizeof(FitTodo) * cnt, hipMemcpyDeviceToHost));
+    // per output entry: every queued region's answer (all must fit for poly_ylop_area), and the
+    // fit mask of the regions that do
+    std::sort(todo.begin(), todo.end(), [](const FitTodo& a, const FitTodo& b) { return a.pos < b.pos; });
+    for (size_t k = 0; k < todo.size();) {
+        const uint64_t pos = todo[k].pos;
+        bool ok = true;
+        uint64_t fm = 0;
+        for (; k < todo.size() && todo[k].pos == pos; ++k) {
+            const int r = host_fit(c, todo[k].q, todo[k].rm);
+            ok &= r == 1;
+            if (r == 1) fm |= 1ull << (todo[k].rid & 63u);
+        }
+        uint16_t b = 0;
+        HIPCHK(c, hipMemcpy(&b, d_bits + pos, sizeof b, hipMemcpyDeviceToHost));
+        b = (uint16_t)(b & ~SPARC_RULE_SEARCH_EXHAUSTED);
+        if (!ok) b = (uint16_t)(b & ~(SPARC_RULE_POLY_YLOP | SPARC_RULE_ALL));
+        HIPCHK(c, hipMemcpy(d_bits + pos, &b, sizeof b, hipMemcpyHostToDevice));
+        if (d_fit && fm) {
+            uint64_t f = 0;
+            HIPCHK(c, hipMemcpy(&f, d_fit + pos, sizeof f, hipMemcpyDeviceToHost));
+            f |= fm;
+            HIPCHK(c, hipMemcpy(d_fit + pos, &f, sizeof f, hipMemcpyHostToDevice));
+        }
+    }
+    return SPARC_OK;
 }
 
 int sparc_rules_host(void* ctx, uint16_t* bits, uint8_t* region, uint64_t* fit) {
@@ -2112,6 +2573,8 @@ int sparc_rules_host(void* ctx, uint16_t* bits, uint8_t* region, uint64_t* fit) 
         HIPCHK(c, hipMalloc(&c->s_fit, 8 * n));
     }
     rc = sparc_rules_device(c, c->s_bits, region ? c->s_region : nullptr, fit ? c->s_fit : nullptr);
+    if (rc) return rc;
+    rc = sparc_rules_finish(c, c->s_bits, fit ? c->s_fit : nullptr);
     if (rc) return rc;
     if (bits) HIPCHK(c, hipMemcpyAsync(bits, c->s_bits, 2 * n, hipMemcpyDeviceToHost, c->stream));
     if (region) HIPCHK(c, hipMemcpyAsync(region, c->s_region, rb, hipMemcpyDeviceToHost, c->stream));
@@ -2230,6 +2693,18 @@ int sparc_copy_state_device(void* ctx, int32_t which, void* d_out) {
 // stream (SURVEY §8b sparc_rccl_gather; the reference is single-process, llm_host.py:257-264).
 // librccl is opened on first use, so the library loads (and the step path runs) without it.
 namespace {
+// The few RCCL declarations the gather uses, as rccl.h (RCCL 2.x ABI) declares them: librccl is
+// dlopen'ed, so neither the library nor its headers are needed to build or load this library.
+typedef struct ncclComm* ncclComm_t;
+typedef struct {
+    char internal[128];
+} ncclUniqueId;
+typedef int ncclResult_t;                           // ncclSuccess = 0, errors > 0
+constexpr ncclResult_t ncclSuccess = 0;
+typedef int ncclDataType_t;
+constexpr ncclDataType_t ncclInt32 = 2;             // rccl.h: ncclInt32 = 2
+static_assert(sizeof(ncclUniqueId) == SPARC_COMM_ID_BYTES, "SPARC_COMM_ID_BYTES is NCCL_UNIQUE_ID_BYTES");
+
 struct Rccl {
     bool tried = false, ok = false;
     std::string why;

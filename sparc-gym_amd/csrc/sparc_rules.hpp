@@ -51,7 +51,28 @@ constexpr int kFitCells = 64;     // cell grid of the exact fit (15 x 15 lattice
 constexpr int kFitYlops = 16;     // per puzzle limits, validated by the loader
 constexpr int kFitShapes = 16;
 constexpr int kFitDepth = 64;
-constexpr uint32_t kFitCap = 1u << 26;   // search nodes before the env's audit reports SPARC_RULE_SEARCH_EXHAUSTED
+// default node cap of one exact-fit search on the GPU (sparc_set_fit_cap): a search that passes it
+// stops, and the host finishes it without a cap (FitQueue below, the C ABI's fallback), so
+// callers see the reference's unbounded answer
+constexpr uint32_t kFitCap = 1u << 26;
+
+// Exact-fit searches that passed the GPU's node cap, handed to the host (sparc_rules_finish runs
+// exact_fit on them without a cap and patches the outputs): the output index of the audit (pos:
+// env, or t * N + env in a rollout), the region's cell mask, the puzzle and the region id.
+struct FitTodo {
+    uint64_t pos;
+    uint64_t rm;
+    uint32_t q, rid;
+};
+struct FitQueue {
+    uint32_t* count;   // entries pushed (may pass cap: the host then reports the overflow)
+    FitTodo* items;
+    uint32_t cap;
+};
+__device__ __forceinline__ void fit_queue_push(const FitQueue& fq, uint64_t pos, uint64_t rm, uint32_t q, uint32_t rid) {
+    const uint32_t k = atomicAdd(fq.count, 1u);
+    if (k < fq.cap) fq.items[k] = FitTodo{pos, rm, q, rid};
+}
 
 struct RulesTab {
     const uint64_t* __restrict__ planes;      // [P][RP_COUNT][W]
@@ -62,12 +83,14 @@ struct RulesTab {
     const int8_t* __restrict__ shape_off;     // [offsets][2] (dcx, dcy) in cell units
     uint32_t num_puzzles;
     uint32_t area;   // 1: the RP_AREA planes hold every cell's net area (else the list is walked)
+    uint32_t fit_cap;   // search nodes of one exact fit before it is handed to the host
     // the per-region check codes (region_code) of every region cell mask of each puzzle with at
     // most kRegTabCells cells, computed once by sparc_load_rules: reg_off[q] = the puzzle's first
     // entry (a multiple of 8) or kNoRegTab; entries of 4 bits, 8 per word of reg_tab.  May be
     // null (no table).
     const uint32_t* __restrict__ reg_off;
     const uint32_t* __restrict__ reg_tab;
+    FitQueue fq;   // count null: no queue (region-table builds: the host scans the table instead)
 };
 constexpr uint32_t kNoRegTab = 0xFFFFFFFFu;
 constexpr uint32_t kRegTabCells = 12;
@@ -75,32 +98,33 @@ constexpr uint32_t kRegTabCells = 12;
 template <int W>
 struct BB {
     uint64_t w[W];
-    __device__ __forceinline__ static BB zero() { BB r; for (int k = 0; k < W; ++k) r.w[k] = 0; return r; }
-    __device__ __forceinline__ static BB load(const uint64_t* p) { BB r; for (int k = 0; k < W; ++k) r.w[k] = p[k]; return r; }
-    __device__ __forceinline__ BB operator&(const BB& o) const { BB r; for (int k = 0; k < W; ++k) r.w[k] = w[k] & o.w[k]; return r; }
-    __device__ __forceinline__ BB operator|(const BB& o) const { BB r; for (int k = 0; k < W; ++k) r.w[k] = w[k] | o.w[k]; return r; }
-    __device__ __forceinline__ BB operator^(const BB& o) const { BB r; for (int k = 0; k < W; ++k) r.w[k] = w[k] ^ o.w[k]; return r; }
-    __device__ __forceinline__ BB andnot(const BB& o) const { BB r; for (int k = 0; k < W; ++k) r.w[k] = w[k] & ~o.w[k]; return r; }
-    __device__ __forceinline__ bool any() const { uint64_t a = 0; for (int k = 0; k < W; ++k) a |= w[k]; return a != 0; }
-    __device__ __forceinline__ bool operator==(const BB& o) const {
+    // (host and device: the host finishes exact-fit searches that pass the GPU's node cap)
+    __host__ __device__ __forceinline__ static BB zero() { BB r; for (int k = 0; k < W; ++k) r.w[k] = 0; return r; }
+    __host__ __device__ __forceinline__ static BB load(const uint64_t* p) { BB r; for (int k = 0; k < W; ++k) r.w[k] = p[k]; return r; }
+    __host__ __device__ __forceinline__ BB operator&(const BB& o) const { BB r; for (int k = 0; k < W; ++k) r.w[k] = w[k] & o.w[k]; return r; }
+    __host__ __device__ __forceinline__ BB operator|(const BB& o) const { BB r; for (int k = 0; k < W; ++k) r.w[k] = w[k] | o.w[k]; return r; }
+    __host__ __device__ __forceinline__ BB operator^(const BB& o) const { BB r; for (int k = 0; k < W; ++k) r.w[k] = w[k] ^ o.w[k]; return r; }
+    __host__ __device__ __forceinline__ BB andnot(const BB& o) const { BB r; for (int k = 0; k < W; ++k) r.w[k] = w[k] & ~o.w[k]; return r; }
+    __host__ __device__ __forceinline__ bool any() const { uint64_t a = 0; for (int k = 0; k < W; ++k) a |= w[k]; return a != 0; }
+    __host__ __device__ __forceinline__ bool operator==(const BB& o) const {
         uint64_t a = 0; for (int k = 0; k < W; ++k) a |= w[k] ^ o.w[k]; return a == 0;
     }
-    __device__ __forceinline__ int popc() const { int s = 0; for (int k = 0; k < W; ++k) s += __popcll(w[k]); return s; }
-    __device__ __forceinline__ bool test(uint32_t b) const { return (w[b >> 6] >> (b & 63)) & 1ull; }
-    __device__ __forceinline__ void set(uint32_t b) { w[b >> 6] |= 1ull << (b & 63); }
+    __host__ __device__ __forceinline__ int popc() const { int s = 0; for (int k = 0; k < W; ++k) s += __builtin_popcountll(w[k]); return s; }
+    __host__ __device__ __forceinline__ bool test(uint32_t b) const { return (w[b >> 6] >> (b & 63)) & 1ull; }
+    __host__ __device__ __forceinline__ void set(uint32_t b) { w[b >> 6] |= 1ull << (b & 63); }
     // lowest set bit index (requires any())
-    __device__ __forceinline__ uint32_t lowest() const {
+    __host__ __device__ __forceinline__ uint32_t lowest() const {
         for (int k = 0; k < W; ++k)
-            if (w[k]) return 64u * k + (uint32_t)__ffsll((long long)w[k]) - 1u;
+            if (w[k]) return 64u * k + (uint32_t)__builtin_ctzll(w[k]);
         return 0;
     }
     // toward higher bit indices by s (0 < s < 64)
-    __device__ __forceinline__ BB shl(uint32_t s) const {
+    __host__ __device__ __forceinline__ BB shl(uint32_t s) const {
         BB r;
         for (int k = W - 1; k >= 0; --k) r.w[k] = (w[k] << s) | (k ? w[k - 1] >> (64 - s) : 0);
         return r;
     }
-    __device__ __forceinline__ BB shr(uint32_t s) const {
+    __host__ __device__ __forceinline__ BB shr(uint32_t s) const {
         BB r;
         for (int k = 0; k < W; ++k) r.w[k] = (w[k] >> s) | (k + 1 < W ? w[k + 1] << (64 - s) : 0);
         return r;
@@ -116,9 +140,10 @@ struct FitIn {
     const int8_t* shape_off;
     uint32_t first, count;   // the puzzle's instance range
     uint32_t CX, CY;         // cell grid
+    uint32_t cap;            // search nodes before the search is handed to the host
 };
-__device__ __forceinline__ FitIn fit_in(const RulesTab& rt, uint32_t ir, uint32_t X, uint32_t Y) {
-    return FitIn{rt.inst, rt.shape_range, rt.shape_off, ir & 0xFFFFu, ir >> 16, (X - 1) / 2, (Y - 1) / 2};
+__host__ __device__ __forceinline__ FitIn fit_in(const RulesTab& rt, uint32_t ir, uint32_t X, uint32_t Y) {
+    return FitIn{rt.inst, rt.shape_range, rt.shape_off, ir & 0xFFFFu, ir >> 16, (X - 1) / 2, (Y - 1) / 2, rt.fit_cap};
 }
 
 // ---------------------------------------------------------------- exact fit (736-838)
@@ -132,16 +157,16 @@ __device__ __forceinline__ FitIn fit_in(const RulesTab& rt, uint32_t ir, uint32_
 constexpr int kFitPlanes = 6;
 struct FitGrid {
     uint64_t p[kFitPlanes];
-    __device__ __forceinline__ void add(uint64_t m) {
+    __host__ __device__ __forceinline__ void add(uint64_t m) {
 #pragma unroll
         for (int i = 0; i < kFitPlanes; ++i) { const uint64_t t = p[i] & m; p[i] ^= m; m = t; }
     }
-    __device__ __forceinline__ void sub(uint64_t m) {
+    __host__ __device__ __forceinline__ void sub(uint64_t m) {
 #pragma unroll
         for (int i = 0; i < kFitPlanes; ++i) { const uint64_t t = ~p[i] & m; p[i] ^= m; m = t; }
     }
-    __device__ __forceinline__ uint64_t neg() const { return p[kFitPlanes - 1]; }
-    __device__ __forceinline__ uint64_t nonzero() const {
+    __host__ __device__ __forceinline__ uint64_t neg() const { return p[kFitPlanes - 1]; }
+    __host__ __device__ __forceinline__ uint64_t nonzero() const {
         uint64_t a = 0;
 #pragma unroll
         for (int i = 0; i < kFitPlanes; ++i) a |= p[i];
@@ -150,7 +175,7 @@ struct FitGrid {
 };
 
 // pattern (relative to the anchor) and fitting anchors of shape `sh` on a CX x CY cell grid
-__device__ __forceinline__ void fit_shape(const FitIn& rt, uint32_t sh, uint32_t CX, uint32_t CY, uint64_t& pat,
+__host__ __device__ __forceinline__ void fit_shape(const FitIn& rt, uint32_t sh, uint32_t CX, uint32_t CY, uint64_t& pat,
                                           uint64_t& va) {
     const uint32_t sr = rt.shape_range[sh];
     const uint32_t o0 = sr & 0xFFFFu, n = sr >> 16;
@@ -214,11 +239,11 @@ __device__ __forceinline__ uint64_t cell_mask_p8(const FitIn& in, uint64_t rc) {
 // _polyfit_region_exact with the area check passed (so net = area > 0 and the grid starts at
 // -1 on the region's cells), as a depth-first search over the same choices (existence only:
 // identical ylops take non-decreasing anchors, polys are tried by distinct shape).  Returns 1 (fits),
-// 0 (does not fit) or -1: the search passed kFitCap nodes without an answer (the env's audit
-// then reports SPARC_RULE_SEARCH_EXHAUSTED; the reference would keep searching).  rm: the
-// region's cells (cell_mask).
-template <int W>
-__device__ __noinline__ int exact_fit(const FitIn in, const BB<W> Rc, uint64_t rm) {
+// 0 (does not fit) or -1: the search passed `cap` nodes without an answer (on the GPU the audit
+// then queues the region for the host, which runs this same function without a cap: the
+// reference's search is unbounded).  rm: the region's cells (cell_mask).
+template <int W, class I = uint32_t>
+__host__ __device__ __noinline__ int exact_fit(const FitIn in, const BB<W> Rc, uint64_t rm, I cap) {
     const FitIn& rt = in;
     const uint32_t CX = in.CX, CY = in.CY;
     FitGrid g;
@@ -251,9 +276,9 @@ __device__ __noinline__ int exact_fit(const FitIn in, const BB<W> Rc, uint64_t r
     const int LMAX = ny + np;
     int L = 0;
     cur[0] = -1;
-    uint32_t iters = 0;
+    I iters = 0;
     while (true) {
-        if (++iters > kFitCap) return -1;
+        if (++iters > cap) return -1;
         if (L < ny) {                                            // _polyfit_place_ylops
             int a = cur[L];
             if (a >= 0) g.add(ypat[L] << a);
@@ -265,7 +290,7 @@ __device__ __noinline__ int exact_fit(const FitIn in, const BB<W> Rc, uint64_t r
                 --L;
                 continue;
             }
-            a = __ffsll((long long)cand) - 1;
+            a = __builtin_ctzll(cand);
             g.sub(ypat[L] << a);
             cur[L] = a;
             cur[++L] = -1;
@@ -286,7 +311,7 @@ __device__ __noinline__ int exact_fit(const FitIn in, const BB<W> Rc, uint64_t r
                 --L;
                 continue;
             }
-            pat[lv] = __ffsll((long long)ng) - 1;               // the first negative cell
+            pat[lv] = __builtin_ctzll(ng);                       // the first negative cell
         } else {
             g.sub(dpat[j] << pat[lv]);
             ++cnt[j];
@@ -410,7 +435,7 @@ __device__ uint32_t region_code(const RulesTab& rt, const FitIn& fin, uint32_t q
             int r = -1;
             if constexpr (!std::is_same<Memo, NoMemo>::value) r = memo->find(q, rm);
             if (r < 0) {
-                r = exact_fit<W>(fin, Rc, rm);
+                r = exact_fit<W>(fin, Rc, rm, fin.cap);
                 if constexpr (!std::is_same<Memo, NoMemo>::value)
                     if (r >= 0) memo->put(q, rm, r);
             }
@@ -459,6 +484,7 @@ template <int W>
 struct PuzzleRules {
     BB<W> pl[10];   // kBasePlanes order
     uint32_t q, fo, tx, ty;
+    uint32_t tbit;  // the target's board bit tx * pitch + ty
     FitIn fin;
 };
 constexpr uint32_t kBasePlanes[10] = {RP_CELLS, RP_LATTICE, RP_GAPS, RP_DOTS, RP_TRI, RP_TRI0, RP_TRI1, RP_TRI2,
@@ -477,27 +503,32 @@ __device__ __forceinline__ PuzzleRules<W> puzzle_rules(const Params& p, const Ru
     r.fo = rt.reg_off ? rt.reg_off[q] : kNoRegTab;
     r.tx = inf.y & 0xFFu;
     r.ty = (inf.y >> 8) & 0xFFu;
+    r.tbit = r.tx * p.pitch + r.ty;
     r.fin = fit_in(rt, ir, X, Y);
     return r;
 }
 
-// vis: path points; x, y: agent; pr: the env's puzzle (puzzle_rules).  region_out (may be
-// null): region id per bit.  memo (FitMemo, or NoMemo): exact-fit answers carried between calls
-// of one lane (puzzles without a region-code table).
-template <int W, class Memo = NoMemo>
-__device__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const PuzzleRules<W>& pr, const BB<W>& vis,
-                            uint32_t x, uint32_t y, uint8_t* region_out, Memo* memo = nullptr) {
+// vis: path points; reached: the agent is on the target (_rule_reached_target 487-495); pr: the
+// env's puzzle (puzzle_rules).  region_out (may be null): region id per bit.  memo (FitMemo, or
+// NoMemo): exact-fit answers carried between calls of one lane (puzzles without a region-code
+// table).  TABLE_ONLY: every region is looked up in the region-code table (the caller checked
+// that the puzzle has one), so no check and no exact-fit search is compiled in.  pos: the index
+// of this audit's outputs, for the FitQueue entry of a search that passes the node cap (its
+// region then counts as passing and the bits carry SPARC_RULE_SEARCH_EXHAUSTED until the host has
+// finished the search; the region-code table never holds such a code after sparc_load_rules).
+template <int W, class Memo = NoMemo, bool TABLE_ONLY = false>
+__device__ RuleOut<W> audit_r(const Params& p, const RulesTab& rt, const PuzzleRules<W>& pr, const BB<W>& vis,
+                              bool reached, uint8_t* region_out, Memo* memo = nullptr, uint64_t pos = 0) {
     const uint32_t q = pr.q, fo = pr.fo;
     const FitIn& fin = pr.fin;
     // the symbol planes only for a puzzle without a region-code table
     BB<W> pl[RP_ABI];
-    if (fo == kNoRegTab) {
+    if (!TABLE_ONLY && fo == kNoRegTab) {
         const uint64_t* g = rt.planes + (size_t)q * RP_COUNT * W;
 #pragma unroll
         for (uint32_t k = RP_STAR; k <= RP_M2; ++k) pl[k] = BB<W>::load(g + k * W);
         pl[RP_INST] = BB<W>::load(g + RP_INST * W);
     }
-    const uint32_t tx = pr.tx, ty = pr.ty;
     const uint32_t P = p.pitch;
     const BB<W> cells = pr.pl[kB_CELLS];
     const BB<W> gaps = pr.pl[kB_GAPS];
@@ -511,7 +542,7 @@ __device__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const PuzzleRul
         star_ok &= (code & kRcStar) != 0;
         const uint32_t poly = code >> kRcPolyShift;
         exhausted |= poly == 3u;
-        poly_ok &= poly < 2u;
+        poly_ok &= poly != 2u;   // 3: passing until the host has finished the search
         if (poly == 1u) fit_ok |= 1ull << (r & 63);
     };
     // a table lookup is consumed one region later, so its L2 latency overlaps the next flood fill
@@ -557,14 +588,16 @@ __device__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const PuzzleRul
             rm = cell_mask<W>(fin, Rc, P);
         if (tpend) take((tw >> tsh) & 15u, trid);
         tpend = false;
-        if (fo != kNoRegTab) {                                   // the precomputed code
+        if (TABLE_ONLY || fo != kNoRegTab) {                     // the precomputed code
             const uint32_t m = (uint32_t)rm;
             tw = rt.reg_tab[(fo + m) >> 3];
             tsh = (m & 7u) * 4u;
             trid = rid;
             tpend = true;
-        } else {
-            take(region_code<W, Memo>(rt, fin, q, Rc, rm, pl, memo), rid);
+        } else if constexpr (!TABLE_ONLY) {
+            const uint32_t code = region_code<W, Memo>(rt, fin, q, Rc, rm, pl, memo);
+            if ((code >> kRcPolyShift) == 3u && rt.fq.count) fit_queue_push(rt.fq, pos, rm, q, rid);
+            take(code, rid);
         }
         ++rid;
     }
@@ -575,7 +608,6 @@ __device__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const PuzzleRul
     const BB<W> n0 = s1 ^ s2, k0 = s1 & s2, n1 = c1 ^ c2 ^ k0, n2 = c1 & c2;
     const BB<W> bad = pr.pl[kB_TRI] & ((n0 ^ pr.pl[kB_TRI0]) | (n1 ^ pr.pl[kB_TRI1]) | (n2 ^ pr.pl[kB_TRI2]));
     const bool tri_ok = !bad.any();
-    const bool reached = x == tx && y == ty;
     const bool gap_ok = !(gaps & vis).any();
     const bool dot_ok = !pr.pl[kB_DOTS].andnot(vis).any();
     uint32_t bits = (uint32_t)reached | 2u | ((uint32_t)gap_ok << 2) | ((uint32_t)dot_ok << 3) |
@@ -584,6 +616,14 @@ __device__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const PuzzleRul
     bits |= (uint32_t)((bits & 0xFFu) == 0xFFu) << 8;
     bits |= (uint32_t)exhausted << 9;
     return RuleOut<W>{bits, fit_ok};
+}
+
+// the audit with the agent at (x, y)
+template <int W, class Memo = NoMemo>
+__device__ __forceinline__ RuleOut<W> audit(const Params& p, const RulesTab& rt, const PuzzleRules<W>& pr,
+                                            const BB<W>& vis, uint32_t x, uint32_t y, uint8_t* region_out,
+                                            Memo* memo = nullptr, uint64_t pos = 0) {
+    return audit_r<W, Memo, false>(p, rt, pr, vis, x == pr.tx && y == pr.ty, region_out, memo, pos);
 }
 
 }  // namespace sparc

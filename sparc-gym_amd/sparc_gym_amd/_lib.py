@@ -54,6 +54,7 @@ _SIGS = {
     "sparc_step_host": ([c_void_p, c_void_p, c_void_p, c_void_p], c_int32),
     "sparc_rollout_device": ([c_void_p, c_int32, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p],
                              c_int32),
+    "sparc_random_actions_device": ([c_void_p, c_int32, c_uint64, c_uint64, c_void_p], c_int32),
     "sparc_obs_pack_device": ([c_void_p, c_void_p, c_void_p, c_int32, c_int32], c_int32),
     "sparc_step_obs_device": ([c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_int32,
                                c_void_p, c_void_p], c_int32),
@@ -71,6 +72,8 @@ _SIGS = {
     "sparc_load_rules": ([c_void_p, ctypes.POINTER(SparcRulesTable)], c_int32),
     "sparc_rules_device": ([c_void_p, c_void_p, c_void_p, c_void_p], c_int32),
     "sparc_rules_host": ([c_void_p, c_void_p, c_void_p, c_void_p], c_int32),
+    "sparc_rules_finish": ([c_void_p, c_void_p, c_void_p], c_int32),
+    "sparc_set_rule_limits": ([c_void_p, ctypes.c_uint32, c_uint64], c_int32),
     "sparc_comm_unique_id": ([c_void_p], c_int32),
     "sparc_comm_init": ([c_void_p, c_int32, c_int32, c_void_p, ctypes.POINTER(c_void_p)], c_int32),
     "sparc_comm_destroy": ([c_void_p], c_int32),

@@ -78,6 +78,16 @@ class SparcCore:
     def rules_device(self, d_bits, d_region=None, d_fit=None):
         self._check(self.lib.sparc_rules_device(self.ctx, d_bits, d_region, d_fit))
 
+    def rules_finish(self, d_bits, d_fit=None):
+        """Finish, on the host and without a node cap, the exact-fit searches of the last audit
+        call that passed the GPU's cap, and patch its bits (and fit) in place (synchronous)."""
+        self._check(self.lib.sparc_rules_finish(self.ctx, d_bits, d_fit))
+
+    def set_rule_limits(self, fit_cap=0, table_entries=0):
+        """GPU node cap of one exact-fit search (0: 2^26) and the region-code table budget in
+        entries (0: 2^28); the budget applies at the next load_rules."""
+        self._check(self.lib.sparc_set_rule_limits(self.ctx, int(fit_cap or 0), int(table_entries or 0)))
+
     def close(self):
         if getattr(self, "ctx", None) is not None and self.ctx.value:
             self.lib.sparc_destroy(self.ctx)
@@ -153,6 +163,11 @@ class SparcCore:
     def rollout_device(self, T, d_actions, d_reward, d_flags, d_stats=None, seed=0, t0=0):
         self._check(self.lib.sparc_rollout_device(self.ctx, int(T), d_actions, int(seed) & (2**64 - 1),
                                                   int(t0), d_reward, d_flags, d_stats))
+
+    def random_actions_device(self, T, d_actions, seed=0, t0=0):
+        """[T, N] uint8 counter-based random actions (global env ids) into device memory."""
+        self._check(self.lib.sparc_random_actions_device(self.ctx, int(T), int(seed) & (2**64 - 1), int(t0),
+                                                         d_actions))
 
     def step_obs_device(self, d_actions, d_reward, d_flags, d_visited, d_agent, x_dim, y_dim, d_puzzle=None,
                         d_xy=None):

@@ -115,7 +115,7 @@ class SPaRC_Gym(Env):
 
     def __init__(self, df_name="lkaesberg/SPaRC", df_split="all", df_set="test", render_mode=None,
                  observation="new", traceback=False, max_steps=2000, puzzles=None, device=0, rule_status=True,
-                 alias_compat=False):
+                 alias_compat=False, fit_cap=None):
         self.render_mode = render_mode
         self.alias_compat = bool(alias_compat)
         self.observation = observation
@@ -132,6 +132,8 @@ class SPaRC_Gym(Env):
         self.puzzles = process_puzzles(df, observation)
         self._core = SparcCore(pack_table(self.puzzles), 1, traceback, max_steps, "none", device)
         self._audit = bool(rule_status)
+        if fit_cap is not None:   # GPU node cap of one exact fit (the host finishes longer searches)
+            self._core.set_rule_limits(fit_cap, 0)
         if self._audit:
             self._core.load_rules(pack_rules(self.puzzles, self._core.table))
         self._legal = 0

@@ -17,7 +17,7 @@ RULE_NAMES = ("reached_target", "path_not_crossing", "no_gap_violations", "all_d
               "square_color_separation", "star_pairing_exact", "triangles_edge_count", "poly_ylop_area",
               "all_rules_satisfied")
 SKIP_LAYERS = ("visited", "gaps", "agent_location", "target_location")
-RULE_SEARCH_EXHAUSTED = 1 << 9   # SPARC_RULE_SEARCH_EXHAUSTED: an exact-fit search hit its node cap
+RULE_SEARCH_EXHAUSTED = 1 << 9   # SPARC_RULE_SEARCH_EXHAUSTED: an exact fit still pending on the host
 
 
 def region_map_of(region_bits, x_size, y_size, pitch):
@@ -31,17 +31,14 @@ def rule_status(puzzle, obs_array, path, agent, target, bits, region_map, fit, t
                 truncated=False):
     """The reference's rule_status dict (structure of SPaRC_Gym.py:896-950).
 
-    The kernel caps each exact-fit search (sparc_rules.hpp kFitCap).  Past the cap the poly/ylop
-    answer is unknown: rather than guess (a dict that silently differs from the reference's) or
-    abort the caller's episode, `poly_ylop_area` and `all_rules_satisfied` then report
-    ``passed=None`` and the poly detail carries ``"search_exhausted": True``."""
-    exhausted = bool(int(bits) & RULE_SEARCH_EXHAUSTED)
+    The GPU caps each exact-fit search; the C ABI finishes any search past the cap on the host
+    without a cap (sparc_rules_finish, run by sparc_rules_host), so `bits` always carry the
+    reference's answer.  Bits that still mark a pending search are a caller error."""
+    if int(bits) & RULE_SEARCH_EXHAUSTED:
+        raise RuntimeError("rule bits with a pending exact-fit search: call sparc_rules_finish first")
     color = np.asarray(puzzle["color_array"])
     add = np.asarray(puzzle["additional_info"])
     passed = {n: bool((int(bits) >> k) & 1) for k, n in enumerate(RULE_NAMES)}
-    if exhausted:
-        passed["poly_ylop_area"] = None
-        passed["all_rules_satisfied"] = None if all(passed[n] for n in RULE_NAMES[:7]) else False
     nreg = int(region_map.max()) + 1 if region_map.size and region_map.max() >= 0 else 0
     # _collect_region_symbols (456-481): per region, layer -> coords and colour -> count
     symbols = [dict() for _ in range(nreg)]
@@ -136,10 +133,7 @@ def rule_status(puzzle, obs_array, path, agent, target, bits, region_map, fit, t
                     if t != req:
                         mism.append({"x": x, "y": y, "required": req, "touches": t})
         add_rule("triangles_edge_count", {"mismatches": mism})
-    poly = _poly_detail(puzzle, obs_array, add, region_map, area, fit)
-    if exhausted:
-        poly["search_exhausted"] = True
-    add_rule("poly_ylop_area", poly)
+    add_rule("poly_ylop_area", _poly_detail(puzzle, obs_array, add, region_map, area, fit))
     core = [k for k in res]
     add_rule("all_rules_satisfied", {"rules_checked": core})
     res["_terminated"] = {"passed": True, "detail": terminated}

@@ -22,7 +22,9 @@ static planes (gaps, target, symbols, color, additional_info) of every puzzle ar
 
 Rule audit (``rules=True``, or ``rule_audit()`` on demand): the reference's
 ``info['rule_status']`` (SPaRC_Gym.py:941-950) evaluated by the k_rules kernel for every env,
-as ``info['rule_bits']`` [N] int16 with bit k = ``RULE_NAMES[k]`` passed.
+as ``info['rule_bits']`` [N] int16 with bit k = ``RULE_NAMES[k]`` passed.  An exact-fit search
+that passes the GPU's node cap (``fit_cap``, default 2^26) is finished on the host without a
+cap, as the reference's unbounded search (sparc_rules_finish): the bits are always final.
 """
 from __future__ import annotations
 
@@ -44,7 +46,8 @@ REWARD_SCALE = 100.0
 class SPaRCVecEnv:
     def __init__(self, num_envs, puzzles=None, df_name="lkaesberg/SPaRC", df_split="all", df_set="test",
                  observation="new", traceback=False, max_steps=2000, autoreset="next_step", device=0,
-                 env_offset=0, pitch=None, words=None, processed=None, table=None, rules=False, copy=True):
+                 env_offset=0, pitch=None, words=None, processed=None, table=None, rules=False, copy=True,
+                 fit_cap=None, rule_table_entries=None):
         if observation not in ("new", "compact"):
             raise ValueError("observation must be 'new' or 'compact' for the vector env")
         self.num_envs = int(num_envs)
@@ -64,6 +67,9 @@ class SPaRCVecEnv:
         self.table = table if table is not None else pack_table(processed, pitch, words)
         self.num_puzzles = self.table.num_puzzles
         self.core = SparcCore(self.table, self.num_envs, traceback, max_steps, autoreset, device, env_offset)
+        # rule-audit limits (tests force the host fallback of the exact fit with a tiny cap)
+        if fit_cap is not None or rule_table_entries is not None:
+            self.core.set_rule_limits(fit_cap or 0, rule_table_entries or 0)
         self.x_dim, self.y_dim = self.table.x_max, self.table.y_max
         n, dev = self.num_envs, self.device
         self._act = torch.empty(n, dtype=torch.uint8, device=dev)
@@ -196,6 +202,8 @@ class SPaRCVecEnv:
             out["fit"] = torch.empty(n, dtype=torch.int64, device=self.device)
         self.core.rules_device(self._rbits.data_ptr(), out["region"].data_ptr() if region else None,
                                out["fit"].data_ptr() if fit else None)
+        # exact fits that passed the GPU's node cap: finished on the host (a sync; no-op otherwise)
+        self.core.rules_finish(self._rbits.data_ptr(), out["fit"].data_ptr() if fit else None)
         return out
 
     @property
@@ -334,6 +342,7 @@ class SPaRCVecEnv:
             self._load_rules()
             bits = torch.empty((T, n), dtype=torch.int16, device=self.device)
             self.core.rollout_rules_device(T, *args, bits.data_ptr(), seed, t0)
+            self.core.rules_finish(bits.data_ptr())   # searches past the GPU's node cap (a sync)
             return {"reward_code": rew, "flags": flags, "rule_bits": bits}
         if not obs and obs_out is None:
             self.core.rollout_device(T, *args, seed, t0)
@@ -351,6 +360,20 @@ class SPaRCVecEnv:
         self.core.rollout_obs_device(T, *args, None if vis is None else vis.data_ptr(),
                                      None if agent is None else agent.data_ptr(), X, Y, seed, t0)
         return {"reward_code": rew, "flags": flags, "visited": vis, "agent_location": agent}
+
+    def random_actions(self, T, seed=0, t0=0, out=None):
+        """[T, N] uint8 uniform random actions written on the GPU: ``action_space.sample()``
+        (Final_Product.py:29) for every env and step, entry (t, i) = sparc_rand_action(seed,
+        env_offset + i, t0 + t) — the actions ``rollout(T, None, seed, t0)`` draws, keyed by the
+        global env id (a rank's shard holds the columns of one process over all envs)."""
+        self._stream()
+        n = self.num_envs
+        if out is None:
+            out = torch.empty((T, n), dtype=torch.uint8, device=self.device)
+        elif out.shape != (T, n) or out.dtype != torch.uint8 or not out.is_contiguous() or out.device != self.device:
+            raise ValueError(f"out must be a contiguous uint8 tensor [{T}, {n}] on {self.device}")
+        self.core.random_actions_device(T, out.data_ptr(), seed, t0)
+        return out
 
     def state(self):
         """Host snapshot of the per-env state (x, y, path_len, step, puzzle, outcome, visited bits)."""

@@ -70,3 +70,13 @@ def test_cpu_bench_covers_every_bench_config():
     from oracle import cpu_bench
     for name, (sizes, full, tb, _obs) in bench.CONFIGS.items():
         assert cpu_bench.CONFIGS[name] == (sizes, full, tb), name
+
+
+def test_rule_config_refuses_step_mode(monkeypatch, capsys):
+    """--mode step runs no rule audit, so a rule config (c3r) in step mode is an argument error,
+    not a line that labels a workload it never ran."""
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--config", "c3r", "--mode", "step"])
+    with pytest.raises(SystemExit) as e:
+        bench.parse()
+    assert e.value.code == 2
+    assert "c3r" in capsys.readouterr().err

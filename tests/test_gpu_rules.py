@@ -32,14 +32,18 @@ def _region_bits(refp, s, pitch, words):
     return out
 
 
+# fit_cap 1: nearly every exact-fit search passes the GPU's node cap and is finished on the host
+# (sparc_rules_finish for the audits, sparc_load_rules for the region-code table), so the answers
+# of the reference's unbounded search (SPaRC_Gym.py:738-853) must come from that fallback
+@pytest.mark.parametrize("fit_cap", [None, 1])
 @pytest.mark.parametrize("pool", RULE_POOLS)
-def test_vec_rules_match_reference(on_gpu, pool):
+def test_vec_rules_match_reference(on_gpu, pool, fit_cap):
     from sparc_gym_amd import SPaRCVecEnv
     g = load(pool)
     eps = g["episodes"]
     n, T = len(eps), max(len(e["actions"]) for e in eps)
     vec = SPaRCVecEnv(n, puzzles=g["records"], traceback=g["traceback"], max_steps=2000, autoreset="none",
-                      rules=True)
+                      rules=True, fit_cap=fit_cap)
     refp = [ref_puzzle(p) for p in g["processed"]]
     pitch, words = vec.table.pitch, vec.table.words
     _, info = vec.reset(options={"puzzle_index": [e["puzzle_index"] for e in eps]})
@@ -61,12 +65,14 @@ def test_vec_rules_match_reference(on_gpu, pool):
             assert np.array_equal(region[i], _region_bits(refp[e["puzzle_index"]], s, pitch, words)), (pool, i, t)
 
 
+@pytest.mark.parametrize("fit_cap", [None, 1])
 @pytest.mark.parametrize("pool", RULE_POOLS)
-def test_single_env_rule_status_matches_reference(on_gpu, pool):
-    """SPaRC_Gym's info['rule_status'] equals the reference's, the whole nested dict."""
+def test_single_env_rule_status_matches_reference(on_gpu, pool, fit_cap):
+    """SPaRC_Gym's info['rule_status'] equals the reference's, the whole nested dict (with the GPU's
+    exact-fit node cap at 1, through the host fallback: never an unknown answer)."""
     from sparc_gym_amd import SPaRC_Gym
     g = load(pool)
-    env = SPaRC_Gym(puzzles=g["records"], traceback=g["traceback"], max_steps=2000)
+    env = SPaRC_Gym(puzzles=g["records"], traceback=g["traceback"], max_steps=2000, fit_cap=fit_cap)
     ids = [r["id"] for r in g["records"]]
     for e, ep in enumerate(g["episodes"][:12]):
         _, info = env.reset(options={"puzzle_id": ids[ep["puzzle_index"]]})
@@ -287,3 +293,83 @@ def test_rules_area_list_fallback_vs_oracle(on_gpu):
             want = rules_ref.rule_bits(rules_ref.audit(p, path, (int(st["x"][i]), int(st["y"][i]))))
             assert int(bits[i]) == want, (T, i)
     vec.core.sync()
+
+
+def _oracle_bits(refp, st, i, pitch):
+    p = refp[int(st["puzzle"][i])]
+    path = _state_points(st["visited"][:, i], pitch, p["x_size"], p["y_size"])
+    return rules_ref.rule_bits(rules_ref.audit(p, path, (int(st["x"][i]), int(st["y"][i]))))
+
+
+def test_exact_fit_fallback_queue_is_used_and_final(on_gpu):
+    """With the GPU's node cap at 1 on a pool without region-code tables (13x13 / 15x15 lattices:
+    the audit runs the memoised search itself), k_rules leaves searches pending
+    (SPARC_RULE_SEARCH_EXHAUSTED) until sparc_rules_finish has run them on the host without a cap;
+    afterwards no bit is pending and every sampled env equals the oracle's audit."""
+    from sparc_gym_amd import SPaRCVecEnv, synthetic
+    from sparc_gym_amd.puzzles import process_puzzles
+    recs = synthetic.make_rule_puzzles(128, seed=11, sizes=((7, 7), (6, 6)), break_prob=0.3)
+    recs += synthetic.make_puzzles(128, seed=12, sizes=((7, 7), (6, 6)), full_properties=True, max_shaped=4)
+    proc = process_puzzles(recs)
+    n = 2048
+    vec = SPaRCVecEnv(n, processed=proc, traceback=True, autoreset="next_step", observation="compact", rules=True,
+                      fit_cap=1)
+    vec.reset(options={"puzzle_index": np.arange(n) % len(proc)})
+    refp = [dict(p) for p in proc]
+    rng = np.random.default_rng(5)
+    pending_seen = 0
+    for T in (0, 6, 25):
+        if T:
+            vec.rollout(T, None, seed=T, record=False)
+        bits = torch.empty(n, dtype=torch.int16, device="cuda")
+        vec.core.rules_device(bits.data_ptr())
+        raw = bits.cpu().numpy().astype(np.uint16)
+        pending_seen += int(((raw >> 9) & 1).sum())
+        vec.core.rules_finish(bits.data_ptr())
+        fin = bits.cpu().numpy().astype(np.uint16)
+        assert not (fin & (1 << 9)).any()
+        st = vec.state()
+        for i in rng.choice(n, size=200, replace=False):
+            assert int(fin[i]) == _oracle_bits(refp, st, i, vec.table.pitch), (T, i)
+    assert pending_seen > 0   # the cap did stop searches on the GPU
+
+
+@pytest.mark.parametrize("budget", [None, 40 * 512])
+@pytest.mark.parametrize("generic", [False, True])
+def test_rules_table_budget_cutoff_mixed_pool(on_gpu, generic, budget, monkeypatch):
+    """budget 40 * 512: a region-code table budget that covers only the first 40 puzzles of a 7x7
+    pool (sparc_load_rules stops at kMaxRegEntries), so the later puzzles are audited by the
+    memoised search and one pool mixes table and search puzzles (the rule rollout then takes the
+    generic kernel k_rollout<1, ..., RULES>).  budget None: every puzzle in the table (k_rollout1r,
+    or with SPARC_RULE_ROLLOUT=generic the generic kernel on the same pool).  With the node cap at 1
+    as well, every step of a rule rollout equals step()-by-step() audits, and samples equal the
+    oracle."""
+    if generic:
+        monkeypatch.setenv("SPARC_RULE_ROLLOUT", "generic")
+    from sparc_gym_amd import SPaRCVecEnv, synthetic
+    from sparc_gym_amd.puzzles import process_puzzles
+    recs = synthetic.make_rule_puzzles(96, seed=21, sizes=((3, 3),), break_prob=0.3)
+    recs += synthetic.make_puzzles(96, seed=22, sizes=((3, 3),), full_properties=True)
+    proc = process_puzzles(recs)
+    n, T = 1024, 20
+    kw = dict(processed=proc, traceback=True, autoreset="next_step", observation="compact", rules=True,
+              max_steps=12, rule_table_entries=budget, fit_cap=1)
+    pids = (np.arange(n) * 7) % len(proc)
+    acts = torch.randint(0, 4, (T, n), dtype=torch.uint8, device="cuda")
+    a = SPaRCVecEnv(n, **kw)
+    a.reset(options={"puzzle_index": pids})
+    ra = a.rollout(T, acts, rules=True)
+    bits = ra["rule_bits"].cpu().numpy().astype(np.uint16)
+    assert not (bits & (1 << 9)).any()
+    c = SPaRCVecEnv(n, **kw)
+    c.reset(options={"puzzle_index": pids})
+    refp = [dict(p) for p in proc]
+    rng = np.random.default_rng(3)
+    for t in range(T):
+        _, _, _, _, info = c.step(acts[t])
+        assert np.array_equal(bits[t], info["rule_bits"].cpu().numpy().astype(np.uint16)), t
+        if t % 5 == 4:
+            st = c.state()
+            for i in rng.choice(n, size=60, replace=False):
+                assert int(bits[t, i]) == _oracle_bits(refp, st, i, c.table.pitch), (t, i)
+    assert len(np.unique(bits)) > 4

@@ -84,10 +84,11 @@ def test_rule_status_layout_matches_reference(pool):
         assert rules_ref.normalize(got) == s["rule_status"], (pool, e, t)
 
 
-def test_exhausted_search_reports_unknown_poly_answer():
-    """An env whose exact-fit search hit the kernel's node cap (SPARC_RULE_SEARCH_EXHAUSTED) gets a
-    rule_status whose poly/ylop answer is marked unknown (passed None, search_exhausted in the
-    detail) instead of a guess, and the call does not abort the caller's episode."""
+def test_pending_exact_fit_bits_are_refused():
+    """SPARC_RULE_SEARCH_EXHAUSTED marks an exact-fit search still pending on the host: the C ABI
+    finishes every search past the GPU's node cap without a cap (sparc_rules_finish, which
+    sparc_rules_host runs itself), so rule_status never sees the flag and never reports an
+    unknown answer (no ``passed: None``); bits that still carry it are a caller error."""
     import numpy as np
     from collections import OrderedDict
     from sparc_gym_amd.rules import RULE_NAMES, RULE_SEARCH_EXHAUSTED, region_map_of, rule_status
@@ -99,12 +100,8 @@ def test_exhausted_search_reports_unknown_poly_answer():
     reg = np.full(64 * table.words, 255, np.uint8)
     args = (p, obs, [list(p["start_location"])], np.array(p["start_location"]), np.array(p["target_location"]))
     rmap = region_map_of(reg, p["x_size"], p["y_size"], table.pitch)
-    # every other core rule passing: all_rules_satisfied is unknown too
-    other = sum(1 << k for k in range(7))
-    rs = rule_status(*args, RULE_SEARCH_EXHAUSTED | other, rmap, 0)
-    assert rs["poly_ylop_area"]["passed"] is None and rs["poly_ylop_area"]["detail"]["search_exhausted"]
-    assert rs["all_rules_satisfied"]["passed"] is None
-    assert all(rs[n]["passed"] is True for n in RULE_NAMES[:7])
-    # a failing core rule decides all_rules_satisfied whatever the poly answer
-    rs = rule_status(*args, RULE_SEARCH_EXHAUSTED | (other & ~1), rmap, 0)
-    assert rs["all_rules_satisfied"]["passed"] is False and rs["poly_ylop_area"]["passed"] is None
+    other = sum(1 << k for k in range(9))
+    with pytest.raises(RuntimeError, match="sparc_rules_finish"):
+        rule_status(*args, RULE_SEARCH_EXHAUSTED | other, rmap, 0)
+    rs = rule_status(*args, other, rmap, 0)
+    assert all(rs[n]["passed"] is True for n in RULE_NAMES)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Kernel-trace stats and the four PMC passes of one rollout workload, for the bench's roofline
 # (run on the GPU box from the repo root; fold the passes here afterwards with
-#  tools/pmc_traffic.py <config>_rollout_n<envs>_chunk<chunk> <kernel> <dir>/pmc_{fetch,write,sq1,sq2}.csv)
+#  tools/pmc_traffic.py <config>_rollout_n<envs>_chunk<chunk> <kernel> <dir>/pmc_{fetch,write,rdreq,sq1,sq2}.csv)
 # usage: tools/collect_profiles.sh <out-dir> <config> <envs> <chunk> [launches]
 set -u
 out=$1; cfg=$2; envs=$3; chunk=$4; launches=${5:-5}
@@ -13,6 +13,7 @@ timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$out/trace" -o run --outp
 f=$(find "$out/trace" -name '*kernel_stats.csv' | head -n 1)
 [ -n "$f" ] && cp "$f" "$out/kernel_stats.csv"
 for pass in "fetch:FETCH_SIZE" "write:WRITE_SIZE" \
+            "rdreq:TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum" \
             "sq1:SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
             "sq2:SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE"; do
     n=${pass%%:*}
@@ -23,5 +24,5 @@ for pass in "fetch:FETCH_SIZE" "write:WRITE_SIZE" \
     f=$(find "$out/$n" -name '*counter_collection.csv' | head -n 1)
     [ -n "$f" ] && cp "$f" "$out/pmc_$n.csv"
 done
-rm -rf "$out/trace" "$out/fetch" "$out/write" "$out/sq1" "$out/sq2"
+rm -rf "$out/trace" "$out/fetch" "$out/write" "$out/rdreq" "$out/sq1" "$out/sq2"
 ls -la "$out"
