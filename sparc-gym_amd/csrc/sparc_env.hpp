@@ -49,7 +49,6 @@ struct Table {
     const uint4* __restrict__ trie;     // [nodes]
     const uint64_t* __restrict__ init;  // [P] padded W = 1 layout: blocked board at reset
     const uint4* __restrict__ row1;     // [P] padded W = 1 layout: compact puzzle row
-    const uint4* __restrict__ trie1;    // [nodes] W = 1 layout: packed nodes (see Env<1>)
     const uint2* __restrict__ trie8;    // [nodes] split-kernel trie records (sparc_trie.hpp)
     const uint2* __restrict__ trieg;    // [nodes][4] record of each node's field-d node (TrieLane::step1la)
     const uint4* __restrict__ trow;     // [P] split-kernel trie rows (sparc_trie.hpp)
@@ -460,7 +459,7 @@ struct Env<1, TB, Stack> {
     // phase_move -> phase_trie hand-over: action, forward / pop, moved on a puzzle with
     // solutions, done, reset step
     uint32_t s_a = 0, s_fwd = 0, s_pop = 0, s_mv = 0, s_done = 0, s_rs = 0;
-    uint4 rec;
+    uint2 rec;
 
     // all arms are computed unconditionally and merged with masks: a C++ ?: whose arms are
     // 64-bit shifts is otherwise lowered to exec-masked if/else blocks
@@ -495,13 +494,15 @@ struct Env<1, TB, Stack> {
         return r.x & 0xFFu;   // start
     }
 
-    // the current node's record, loaded unconditionally (L2-resident table).  W = 1 records
-    // (trie1): x = child[right] | child[up] << 16, y = child[left] | child[down] << 16,
-    // z = parent, each a packed node (index | terminal << 15, 0xFFFF = none).  node <= trie_max
-    // holds on validated tables; the clamp keeps a broken state from reading out of bounds.
+    // the current node's record, loaded unconditionally (L2-resident table): the split
+    // kernels' 8-B records (trie8, sparc_trie.hpp): field d = the child in direction d as a packed
+    // node (index | terminal << 15, 0xFFFF = none), and the PARENT in the field of the direction
+    // back to it, which is exactly the direction a traceback pop moves, so a forward move and a
+    // pop read the same field[action].  node <= trie_max holds on validated tables; the clamp
+    // keeps a broken state from reading out of bounds.
     __device__ __forceinline__ void load_rec(const Params& p) {
         const uint32_t node = nn & 0x7FFFu;
-        rec = p.tab.trie1[trie_base + (node < trie_max ? node : trie_max)];
+        rec = p.tab.trie8[trie_base + (node < trie_max ? node : trie_max)];
     }
 
     // _load_puzzle (SPaRC_Gym.py:166-187) with fresh planes: the puzzle rows and the board,
@@ -599,14 +600,14 @@ struct Env<1, TB, Stack> {
         nn = pick(s_rs != 0u, ((pflags >> 3) & 1u) << 15, nn);
         off = pick(s_rs != 0u, ((pflags >> 1) & 1u) ^ 1u, off);
         // solution trie (first read of the record loaded at the previous step): a forward move
-        // on the trie goes to the child (or leaves the trie), a pop on the trie to the parent,
-        // off the trie they count the depth off it
+        // on the trie goes to the child field[a] (or leaves the trie), a pop on the trie to the
+        // parent, which is field[a] as well; off the trie they count the depth off it
         const bool on = off == 0;
         const uint32_t c = (uint32_t)((((uint64_t)rec.y << 32) | rec.x) >> ((s_a << 4) & 63u)) & 0xFFFFu;
         const bool has = c != 0xFFFFu;
         const bool down = (s_fwd != 0u) & on & has;
         const bool up = (s_pop != 0u) & on;
-        nn = pick(down, c, pick(up, rec.z, nn));
+        nn = pick(down | up, c, nn);
         off = pick(on, s_fwd & (uint32_t)!has, off + s_fwd - s_pop);
         // the record changes only with the node (a random walk is off the trie on most steps)
         load_rec(p);

@@ -1363,7 +1363,7 @@ struct Ctx {
     uint64_t *vis = nullptr, *dirs = nullptr;
     uint32_t *pos = nullptr, *aux = nullptr, *step = nullptr, *pid = nullptr;
     uint64_t* t_open = nullptr;
-    uint4 *t_info = nullptr, *t_root = nullptr, *t_trie = nullptr, *t_trie1 = nullptr;
+    uint4 *t_info = nullptr, *t_root = nullptr, *t_trie = nullptr;
     uint64_t* t_init = nullptr;
     uint4* t_row1 = nullptr;
     uint2* t_trie8 = nullptr;          // split-kernel tables (null: a puzzle's trie exceeds 15-bit nodes)
@@ -1388,6 +1388,7 @@ struct Ctx {
     int8_t* r_shape_off = nullptr;
     FitMemo<kMemo>* r_memo = nullptr;   // [N] per-env exact-fit memo of the audit (zeroed at sparc_load_rules)
     uint32_t *r_reg_off = nullptr, *r_reg_tab = nullptr;   // region-code table (sparc_rules.hpp)
+    uint64_t* r_rows = nullptr;   // the audit's per-puzzle rows (RulesTab::rows)
     bool r_tab_all = false;   // every puzzle has a region-code table (k_rollout1r's audit)
     bool ring_ok = false;     // W = 1 and every board fits below kRingShift (k_rollout1r's ring word)
     bool rules_generic = false;   // SPARC_RULE_ROLLOUT=generic: rule rollouts on k_rollout<..., RULES> (A/B, tests)
@@ -1443,7 +1444,6 @@ Params make_params(const Ctx* c) {
     p.tab.info = c->t_info;
     p.tab.root = c->t_root;
     p.tab.trie = c->t_trie;
-    p.tab.trie1 = c->t_trie1;
     p.tab.init = c->t_init;
     p.tab.row1 = c->t_row1;
     p.tab.trie8 = c->t_trie8;
@@ -1534,6 +1534,7 @@ RulesTab rules_tab(const Ctx* c, bool queue) {
     rt.reg_off = c->r_reg_off;
     rt.reg_tab = c->r_reg_tab;
     rt.fq = FitQueue{queue ? c->fq_count : nullptr, c->fq_items, kFitQueueCap};
+    rt.rows = c->r_rows;
     return rt;
 }
 
@@ -1622,9 +1623,9 @@ int sparc_destroy(void* ctx) {
     if (!c) return SPARC_OK;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void* bufs[] = {c->vis, c->dirs, c->pos, c->aux, c->step, c->pid, c->t_open, c->t_info, c->t_root, c->t_trie, c->t_trie1, c->t_init, c->t_row1,
+    void* bufs[] = {c->vis, c->dirs, c->pos, c->aux, c->step, c->pid, c->t_open, c->t_info, c->t_root, c->t_trie, c->t_init, c->t_row1,
                     c->t_trie8, c->t_trow, c->t_mrow, c->t_mroww, c->t_boardw, c->err, c->s_act, c->s_flags, c->s_mask, c->s_rew, c->s_pidx, c->r_planes, c->r_inst_range,
-                    c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off, c->r_memo, c->s_bits, c->s_region, c->s_fit, c->r_reg_off, c->r_reg_tab, c->fq_count, c->fq_items};
+                    c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off, c->r_memo, c->s_bits, c->s_region, c->s_fit, c->r_reg_off, c->r_reg_tab, c->fq_count, c->fq_items, c->r_rows};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->own) (void)hipStreamDestroy(c->own);
@@ -1712,8 +1713,6 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
     if (c->t_open) HIPCHK(c, hipFree(c->t_open));
     if (c->t_info) HIPCHK(c, hipFree(c->t_info));
     if (c->t_trie) HIPCHK(c, hipFree(c->t_trie));
-    if (c->t_trie1) HIPCHK(c, hipFree(c->t_trie1));
-    c->t_trie1 = nullptr;
     if (c->t_root) HIPCHK(c, hipFree(c->t_root));
     if (c->t_init) HIPCHK(c, hipFree(c->t_init));
     if (c->t_row1) HIPCHK(c, hipFree(c->t_row1));
@@ -1791,22 +1790,6 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
     HIPCHK(c, hipMemset(c->t_trie, 0xFF, sizeof(uint4) * nn));
     if (t->num_nodes > 0)
         HIPCHK(c, hipMemcpy(c->t_trie, t->trie, sizeof(uint4) * (size_t)t->num_nodes, hipMemcpyHostToDevice));
-    if (W == 1) {
-        // packed-node records of Env<1>: every child and the parent as index | terminal << 15
-        // (0xFFFF = none), so one 16-bit field carries both a node and its terminal flag
-        std::vector<uint4> t1(nn, make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFu, 0u));
-        for (size_t k = 0; k < (size_t)t->num_nodes; ++k) {
-            const uint32_t* r = t->trie + 4 * k;
-            uint32_t ch[4] = {r[0] & 0xFFFFu, r[0] >> 16, r[1] & 0xFFFFu, r[1] >> 16};
-            for (int d = 0; d < 4; ++d)
-                if (ch[d] != 0xFFFFu) ch[d] |= ((r[2] >> (17 + d)) & 1u) << 15;
-            uint32_t par = r[2] & 0xFFFFu;
-            if (par != 0xFFFFu) par |= ((r[2] >> 21) & 1u) << 15;
-            t1[k] = make_uint4(ch[0] | (ch[1] << 16), ch[2] | (ch[3] << 16), par, 0u);
-        }
-        HIPCHK(c, hipMalloc(&c->t_trie1, sizeof(uint4) * nn));
-        HIPCHK(c, hipMemcpy(c->t_trie1, t1.data(), sizeof(uint4) * nn, hipMemcpyHostToDevice));
-    }
     // split-kernel tables (sparc_trie.hpp): 8-B records, field d = the child in direction d,
     // and the parent in the field of the direction back to it (the reverse of the move that
     // reached the node: no reachable child lives there, as that point is on the path); per
@@ -2362,12 +2345,12 @@ int sparc_load_rules(void* ctx, const sparc_rules_table* t) {
         }
     }
     void* old[] = {c->r_planes, c->r_inst_range, c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off,
-                   c->r_reg_off, c->r_reg_tab};
+                   c->r_reg_off, c->r_reg_tab, c->r_rows};
     for (void* b : old)
         if (b) HIPCHK(c, hipFree(b));
     c->r_planes = nullptr; c->r_inst_range = nullptr; c->r_inst = nullptr;
     c->r_shape_range = nullptr; c->r_shape_area = nullptr; c->r_shape_off = nullptr;
-    c->r_reg_off = nullptr; c->r_reg_tab = nullptr;
+    c->r_reg_off = nullptr; c->r_reg_tab = nullptr; c->r_rows = nullptr;
     c->rules = false;
     c->r_tab_all = false;
     // the device copy: the caller's SPARC_RULE_PLANES planes per puzzle, RP_INST rewritten from the
@@ -2485,6 +2468,20 @@ int sparc_load_rules(void* ctx, const sparc_rules_table* t) {
             }
             HIPCHK(c, hipMemcpy(c->r_reg_tab, tab.data(), sizeof(uint32_t) * words, hipMemcpyHostToDevice));
         }
+    }
+    // the audit's per-puzzle rows (RulesTab::rows): base planes, table offset, instance range, info
+    {
+        const size_t RW = W == 1 ? rule_row_u64<1>() : W == 2 ? rule_row_u64<2>() : rule_row_u64<4>();
+        std::vector<uint64_t> rows(P * RW, 0ull);
+        for (size_t q = 0; q < P; ++q) {
+            uint64_t* r = rows.data() + q * RW;
+            for (int k = 0; k < 10; ++k)
+                for (int w = 0; w < W; ++w) r[k * W + w] = dev_planes[(q * RP_COUNT + kBasePlanes[k]) * W + w];
+            r[10 * W] = (uint64_t)reg_off[q] | ((uint64_t)t->inst_range[q] << 32);
+            r[10 * W + 1] = (uint64_t)info[q].x | ((uint64_t)info[q].y << 32);
+        }
+        HIPCHK(c, hipMalloc(&c->r_rows, sizeof(uint64_t) * rows.size()));
+        HIPCHK(c, hipMemcpy(c->r_rows, rows.data(), sizeof(uint64_t) * rows.size(), hipMemcpyHostToDevice));
     }
     c->rules = true;
     return SPARC_OK;

@@ -91,7 +91,14 @@ struct RulesTab {
     const uint32_t* __restrict__ reg_off;
     const uint32_t* __restrict__ reg_tab;
     FitQueue fq;   // count null: no queue (region-table builds: the host scans the table instead)
+    // [P][rule_row_u64<W>()]: what an audit reads when its env changes puzzle, in one contiguous
+    // record (puzzle_rules): the kBasePlanes planes, then reg_off | inst_range << 32, then the
+    // puzzle's info words x | y << 32 (W = 1: 96 B; the planes alone are spread over 264 B of the
+    // plane table)
+    const uint64_t* __restrict__ rows;
 };
+template <int W>
+__host__ __device__ constexpr uint32_t rule_row_u64() { return 10u * W + 2u; }
 constexpr uint32_t kNoRegTab = 0xFFFFFFFFu;
 constexpr uint32_t kRegTabCells = 12;
 
@@ -493,16 +500,17 @@ enum : uint32_t { kB_CELLS = 0, kB_LATTICE, kB_GAPS, kB_DOTS, kB_TRI, kB_TRI0, k
 template <int W>
 __device__ __forceinline__ PuzzleRules<W> puzzle_rules(const Params& p, const RulesTab& rt, uint32_t q) {
     PuzzleRules<W> r;
-    const uint64_t* g = rt.planes + (size_t)q * RP_COUNT * W;
+    const uint64_t* g = rt.rows + (size_t)q * rule_row_u64<W>();
 #pragma unroll
-    for (int k = 0; k < 10; ++k) r.pl[k] = BB<W>::load(g + kBasePlanes[k] * W);
-    const uint4 inf = p.tab.info[q];
-    const uint32_t X = inf.x & 0xFFu, Y = (inf.x >> 8) & 0xFFu;
-    const uint32_t ir = rt.inst_range[q];
+    for (int k = 0; k < 10; ++k) r.pl[k] = BB<W>::load(g + k * W);
+    const uint64_t m0 = g[10 * W], m1 = g[10 * W + 1];
+    const uint32_t ix = (uint32_t)m1, iy = (uint32_t)(m1 >> 32);
+    const uint32_t X = ix & 0xFFu, Y = (ix >> 8) & 0xFFu;
+    const uint32_t ir = (uint32_t)(m0 >> 32);
     r.q = q;
-    r.fo = rt.reg_off ? rt.reg_off[q] : kNoRegTab;
-    r.tx = inf.y & 0xFFu;
-    r.ty = (inf.y >> 8) & 0xFFu;
+    r.fo = (uint32_t)m0;
+    r.tx = iy & 0xFFu;
+    r.ty = (iy >> 8) & 0xFFu;
     r.tbit = r.tx * p.pitch + r.ty;
     r.fin = fit_in(rt, ir, X, Y);
     return r;

@@ -47,12 +47,16 @@ ovis = oag = None
 if obs:   # c4: 'new' observation traces [chunk, N, x_dim, y_dim] int32, as bench.py
     ovis = torch.empty((a.chunk, a.envs, vec.x_dim, vec.y_dim), dtype=torch.int32, device="cuda")
     oag = torch.empty_like(ovis)
+bits = torch.empty((a.chunk, a.envs), dtype=torch.int16, device="cuda") if a.rules else None
+if a.rules:
+    vec._stream()
 ms = []
 for k in range(a.launches + 1):      # first launch = warmup
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    if a.rules:
-        vec.rollout(a.chunk, None if a.rand else acts[k], stats=stats, seed=k, rules=True)
+    if a.rules:   # the bench's direct C-ABI call (rollout(rules=True) would add a host sync per launch)
+        vec.core.rollout_rules_device(a.chunk, None if a.rand else acts[k].data_ptr(), rew.data_ptr(), flg.data_ptr(),
+                                      stats.data_ptr(), bits.data_ptr(), seed=k)
     elif a.no_out:
         vec.rollout(a.chunk, None if a.rand else acts[k], stats=stats, record=False, seed=k)
     else:
