@@ -433,7 +433,9 @@ def main():
     K, W = max(1, args.steps), max(0, args.warmup)
     # env-steps per env in one bench step (one launch)
     rules = args.config in RULE_CONFIGS
-    T = 1 if args.mode == "step" else (args.chunk if args.chunk > 0 else (50 if obs or rules else 2000))
+    # env-steps per launch: 2,000 (as c3; c3r too: its step + audit waves fill a pipeline of
+    # 10-step tiles per launch), 50 with observation traces (c4: 12.7 GB of planes per launch)
+    T = 1 if args.mode == "step" else (args.chunk if args.chunk > 0 else (50 if obs else 2000))
     chunk = T
     # observation traces [T, N, x_dim, y_dim] int32 (visited, agent_location), reused by every
     # launch (a consumer reads them between launches)

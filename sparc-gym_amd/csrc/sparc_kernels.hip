@@ -1392,7 +1392,7 @@ struct Ctx {
     bool r_tab_all = false;   // every puzzle has a region-code table (k_rollout1r's audit)
     bool ring_ok = false;     // W = 1 and every board fits below kRingShift (k_rollout1r's ring word)
     bool rules_generic = false;   // SPARC_RULE_ROLLOUT=generic: rule rollouts on k_rollout<..., RULES> (A/B, tests)
-    int r1r_shape = 0;            // SPARC_R1R_SHAPE: k_rollout1r's <G, A, RT> (0: <4, 3, 12>; A/B, tests)
+    int r1r_shape = 0;            // SPARC_R1R_SHAPE: k_rollout1r's <G, A, RT> (0: <2, 5, 10>; 1, 2: A/B, tests)
     // exact-fit searches past the GPU's node cap (sparc_set_fit_cap) are finished on the host
     // from these copies of the rule table (sparc_rules.hpp exact_fit, the same code)
     uint32_t fit_cap = kFitCap;
@@ -2114,11 +2114,14 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
             if (c->cfg.traceback) go(std::true_type{});
             else go(std::false_type{});
         };
+        // <2, 5, 10>: 128 envs, 2 step + 10 audit waves per workgroup, two workgroups per CU (six
+        // waves per SIMD at 66-80 VGPRs); MI355X, c3r, 50-step launches at 65,536 envs: 0.1245 ms
+        // against 0.1338 for <4, 3, 12> (one 16-wave workgroup per CU, its LDS) and 0.1275 for
+        // <2, 4, 12> (profiles/r04/ab_run2)
         switch (c->r1r_shape) {
-            case 1: go_shape(R1Shape<2, 5, 10>{}); break;
-            case 2: go_shape(R1Shape<4, 2, 16>{}); break;
-            case 3: go_shape(R1Shape<2, 4, 12>{}); break;
-            default: go_shape(R1Shape<4, 3, 12>{}); break;
+            case 1: go_shape(R1Shape<4, 3, 12>{}); break;
+            case 2: go_shape(R1Shape<2, 4, 12>{}); break;
+            default: go_shape(R1Shape<2, 5, 10>{}); break;
         }
         if (lds_rc) return lds_rc;
         return launch_check(c);

@@ -170,10 +170,14 @@ struct TrieLane {
             hs = (int32_t)((nx.w >> 14) & 1u);
             hsn = -hs;
             tmax = nx.w >> 17;
+            // the row of the next reset, read here into the same registers, so nothing waits for
+            // it until that reset (at least two steps later); the empty asm keeps the uses of the
+            // old row above the read (else the compiler lands the read in temporaries and waits
+            // for it right here to copy it into nx).  MI355X, c3: 0.4003-0.4014 -> 0.3950-0.3962
+            // ms per 2,000-step launch against the read on every step (profiles/r04/ab_run2)
+            __asm__ volatile("" ::: "memory");
+            nx = trow[npid];
         }
-        // the row of the next reset, read every step outside the branch: read inside it, the
-        // compiler lands it in temporaries and waits for it right there to copy it into nx
-        nx = trow[npid];
         // forward move or pop on the trie: field[action] (a child, or the parent).  key has
         // bits above 15 set when the lane is off the trie or did not move, so one compare
         // decides; off the trie (or without a child) the move counts the depth instead.

@@ -381,3 +381,41 @@ def test_rules_table_budget_cutoff_mixed_pool(on_gpu, generic, budget, monkeypat
             for i in rng.choice(n, size=60, replace=False):
                 assert int(bits[t, i]) == _oracle_bits(refp, st, i, c.table.pitch), (t, i)
     assert len(np.unique(bits)) > 4
+
+
+@pytest.mark.parametrize("shape", [1, 2])
+def test_rule_rollout_shapes_equal_default(on_gpu, shape, monkeypatch):
+    """Every compiled shape of the W = 1 rule rollout (SPARC_R1R_SHAPE: k_rollout1r <G, A, RT> =
+    <4, 3, 12> and <2, 4, 12> besides the default <2, 5, 10>) gives the same
+    reward codes, flags, stats, rule bits and final state as the default shape (oracle-pinned by
+    test_rollout_rules_c3r_full_size), over two launches (the second with a partial last tile) on
+    a ragged batch (a partial last group)."""
+    from sparc_gym_amd import SPaRCVecEnv, synthetic
+    from sparc_gym_amd.puzzles import process_puzzles
+    recs = synthetic.make_rule_puzzles(128, seed=31, sizes=((3, 3),), break_prob=0.3)
+    recs += synthetic.make_puzzles(128, seed=32, sizes=((3, 3),), full_properties=True)
+    proc = process_puzzles(recs)
+    n, T1, T2 = 8192 + 96, 48, 29
+    kw = dict(processed=proc, traceback=True, autoreset="next_step", observation="compact", rules=True,
+              max_steps=40)
+    pids = (np.arange(n) * 13) % len(proc)
+    acts = torch.randint(0, 5, (T1 + T2, n), dtype=torch.uint8, device="cuda")
+
+    def run():
+        v = SPaRCVecEnv(n, **kw)
+        v.reset(options={"puzzle_index": pids})
+        st = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
+        r1 = v.rollout(T1, acts[:T1], rules=True, stats=st)
+        r2 = v.rollout(T2, acts[T1:], rules=True, stats=st)
+        s = v.state()
+        return [torch.cat([r1[k], r2[k]]).cpu().numpy() for k in ("reward_code", "flags", "rule_bits")], st.cpu().numpy(), s
+
+    want, wst, ws = run()
+    monkeypatch.setenv("SPARC_R1R_SHAPE", str(shape))
+    got, gst, gs = run()
+    for a, b in zip(got, want):
+        assert np.array_equal(a, b)
+    assert np.array_equal(gst, wst)
+    for k in ("x", "y", "path_len", "step", "puzzle", "outcome", "pending", "visited"):
+        assert np.array_equal(gs[k], ws[k]), k
+    assert len(np.unique(want[2])) > 4

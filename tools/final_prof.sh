@@ -9,7 +9,7 @@ if [ "${SKIP_TESTS:-0}" != 1 ]; then
   grep -q " passed" gpurun_out/gputests.log && ! grep -q "failed" gpurun_out/gputests.log || { echo "tests failed"; exit 1; }
   step smoke 120 python -c "import __graft_entry__ as g; g.smoke()"
 fi
-for spec in ${PROF_SPECS:-"c3:65536:2000:k_rollout1s" "c2:4096:2000:k_rollout1s" "c3r:65536:50:k_rollout1r" "c3g7:65536:2000:k_rolloutWs" "c4c:262144:2000:k_rolloutWs" "c4:262144:50:k_rollout"}; do
+for spec in ${PROF_SPECS:-"c3:65536:2000:k_rollout1s" "c2:4096:2000:k_rollout1s" "c3r:65536:2000:k_rollout1r" "c3g7:65536:2000:k_rolloutWs" "c4c:262144:2000:k_rolloutWs" "c4:262144:50:k_rollout"}; do
   IFS=: read cfg envs chunk kern <<< "$spec"
   step prof_$cfg 420 bash tools/collect_profiles.sh gpurun_out/prof_$cfg $cfg $envs $chunk 5
   d=gpurun_out/prof_$cfg

@@ -5,9 +5,9 @@ region-code table on the GPU (k_region_table: every region cell mask of every pu
 
     python tools/prof_load_rules.py [--puzzles 100000] [--distinct 2000] [--grid 3 4]
 
-`--distinct` synthetic puzzles of the given cell grid (3 x 4 cells: 12 cells, 4,096 masks each)
-are generated and repeated up to `--puzzles` (the table build does the same work per puzzle
-whether or not two puzzles are equal).  Prints one JSON line: host packing time, the
+`--distinct` synthetic puzzles of the given cell grid (3 x 4 cells: 12 cells, 4,096 masks each),
+with the full property set and with base planes only, are repeated up to `--full` and
+`--puzzles` (the table build does the same work per puzzle whether or not two are equal).  Prints one JSON line: host packing time, the
 sparc_load_rules wall time, the puzzles that got a table (the rest: past the budget) and the
 entries built."""
 import argparse
@@ -28,12 +28,17 @@ from sparc_gym_amd.puzzles import pack_rules, pack_table, process_puzzles  # noq
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--puzzles", type=int, default=100000)
-ap.add_argument("--distinct", type=int, default=2000)
+ap.add_argument("--distinct", type=int, default=1000)
+ap.add_argument("--full", type=int, default=20000,
+                help="puzzles with the full property set (the rest: base planes); the rule table's "
+                     "instance index is 16 bits, so all puzzles together hold < 65,536 poly/ylop instances")
 ap.add_argument("--grid", type=int, nargs=2, default=(3, 4))
 a = ap.parse_args()
 t0 = time.perf_counter()
-proc = process_puzzles(synthetic.make_puzzles(a.distinct, seed=0, sizes=(tuple(a.grid),), full_properties=True))
-proc = [proc[k % len(proc)] for k in range(a.puzzles)]
+full = process_puzzles(synthetic.make_puzzles(a.distinct, seed=0, sizes=(tuple(a.grid),), full_properties=True))
+base = process_puzzles(synthetic.make_puzzles(a.distinct, seed=1, sizes=(tuple(a.grid),), full_properties=False))
+proc = [full[k % len(full)] for k in range(min(a.full, a.puzzles))]
+proc += [base[k % len(base)] for k in range(a.puzzles - len(proc))]
 t1 = time.perf_counter()
 table = pack_table(proc)
 rules = pack_rules(proc, table)
@@ -48,7 +53,8 @@ t4 = time.perf_counter()
 cells = a.grid[0] * a.grid[1]
 per = 8 * (1 if cells <= 3 else 1 << (cells - 3))
 tabled = min(a.puzzles, (1 << 28) // per)
-print(json.dumps({"puzzles": a.puzzles, "distinct": a.distinct, "cells": cells, "words": table.words,
+print(json.dumps({"puzzles": a.puzzles, "full_property_puzzles": min(a.full, a.puzzles), "distinct": a.distinct,
+                  "cells": cells, "words": table.words, "instances": int(len(rules.inst)),
                   "generate_s": round(t1 - t0, 2), "pack_s": round(t2 - t1, 2),
                   "load_rules_s": round(t4 - t3, 3), "puzzles_with_table": tabled,
                   "table_entries": tabled * per, "table_mb": round(tabled * per / 2 / 2**20, 1)}))
