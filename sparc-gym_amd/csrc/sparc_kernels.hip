@@ -942,17 +942,17 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
 // waves of its own: per 64 envs one STEP wave (Env<1>::advance: the step, the stats, the outputs)
 // and A AUDIT waves, audit wave q auditing the steps t with t % A == q.  Nothing is
 // computed twice and no audit wave carries step state.
-//   The step wave hands every env-step over as ONE u64 in an LDS ring: the visited board (the
-// bits below kRingShift: every W = 1 pool with x_size * pitch <= 57) | the agent's bit << 57 |
-// autoreset << 63.  The audit wave follows the puzzle index through the autoresets itself (a
-// reset loads (index + 1) % P, 1087) and keeps the puzzle's rule planes in registers while it
-// stays on a puzzle.
+//   The step wave hands every env-step over as one u64 and one u32 in LDS rings: the visited
+// board (the bits below kRingShift: every W = 1 pool with x_size * pitch <= 57) | the agent's bit
+// << 57, and the puzzle index after the step | the path rules' bits << 24 (audit_path: reached,
+// gaps, dots, triangles need no regions, so the step wave, off the critical path, decides them).
+// An audit wave reads only its own steps and keeps the puzzle's rule row in registers while its
+// env stays on a puzzle.
 //   Per workgroup 64 * G envs = G step waves (0..G-1) + G * A audit waves (group g = wave % G);
 // tiles of RT steps, one barrier per tile.  In interval k the step waves step tile k and store
 // the rewards / flags of tile k-1 and the rule bits of tile k-2 (whole 16-B pieces of the
-// workgroup's rows), the audit waves audit tile k-1.  The
-// state is only read before B_0 and written after the last barrier, so the audit waves' initial
-// puzzle index is never a later one.
+// workgroup's rows), the audit waves audit tile k-1.  Only the step waves read and write the env
+// state.
 // Shape <G, A, RT>: G 64-env groups per workgroup, A audit waves per group (so G * (1 + A) waves
 // <= 16), RT steps per tile (a multiple of A).
 template <int G, int A, int RT>
@@ -961,7 +961,8 @@ struct R1Geom {
     static constexpr int kBlock = 64 * G * (1 + A);
     static constexpr uint32_t kEnvs = 64u * G;                            // envs per workgroup (a tile row)
     static constexpr size_t kRing = 0;                                      // [2][RT][kEnvs] u64
-    static constexpr size_t kRew = kRing + 2 * RT * kEnvs * 8;             // [2][RT][kEnvs] reward codes
+    static constexpr size_t kPid = kRing + 2 * RT * kEnvs * 8;             // [2][RT][kEnvs] u32 puzzle index
+    static constexpr size_t kRew = kPid + 2 * RT * kEnvs * 4;              // [2][RT][kEnvs] reward codes
     static constexpr size_t kFlg = kRew + 2 * RT * kEnvs;                  // [2][RT][kEnvs] flags
     static constexpr size_t kBits = kFlg + 2 * RT * kEnvs;                 // [2][RT][kEnvs] u16 rule bits
     static constexpr size_t kAct = kBits + 2 * RT * kEnvs * 2;             // [G][RT][64] actions of the tile
@@ -969,6 +970,7 @@ struct R1Geom {
     static constexpr size_t kBase = kStk + (size_t)G * 64 * 64;            // then the W = 1 puzzle rows
 };
 constexpr uint32_t kRingShift = 57;
+constexpr uint32_t kPidBits = 24;   // the puzzle-index ring word: index | path-rule bits << 24
 
 template <bool TB, bool RAND, bool LDS_TABLE, int G, int A, int RT>
 __global__ void __launch_bounds__(64 * G * (1 + A))
@@ -988,6 +990,7 @@ __global__ void __launch_bounds__(64 * G * (1 + A))
     const bool full = tiled && (size_t)wg_base + E <= n;         // block-uniform: 16-B row pieces
     const int32_t K = (T + RT - 1) / RT;
     uint64_t* ring = reinterpret_cast<uint64_t*>(smem + Geo::kRing);
+    uint32_t* rpid = reinterpret_cast<uint32_t*>(smem + Geo::kPid);
     uint8_t* trw = smem + Geo::kRew;
     uint8_t* tfl = smem + Geo::kFlg;
     uint16_t* tbt = reinterpret_cast<uint16_t*>(smem + Geo::kBits);
@@ -1016,6 +1019,8 @@ __global__ void __launch_bounds__(64 * G * (1 + A))
         uint8_t* ta = smem + Geo::kAct + g * (RT * 64u);
         const uint32_t r = lane >> 2, c = (lane & 3u) * 16u;    // this lane's 16-B piece of an action tile
         const bool tact = !RAND && full;                         // actions through the tile prefetch
+        PuzzleRules<1> spr;   // the env's puzzle rules, for the path rules this wave decides
+        spr.q = 0xFFFFFFFFu;
         u32x4 anext = {0u, 0u, 0u, 0u};
         if (tact && (int32_t)r < tile_cnt(0)) anext = nt_load16(act + (size_t)r * n + wg_base + g * 64u + c);
         // tile kt's rewards / flags, or rule bits, from LDS to HBM by the E step-wave lanes
@@ -1073,6 +1078,7 @@ __global__ void __launch_bounds__(64 * G * (1 + A))
                 uint32_t f = 0;
                 int code = 0;
                 uint64_t w = 0;
+                uint32_t q_after = 0;
                 if (active) {
                     code = e.advance(p, src, a, f);
                     acc.x += code;
@@ -1082,9 +1088,15 @@ __global__ void __launch_bounds__(64 * G * (1 + A))
                     uint64_t v[1];
                     uint32_t ab;
                     e.obs_words(p, src, v, ab);
-                    w = v[0] | ((uint64_t)(ab | (((f >> 6) & 1u) << 6)) << kRingShift);
+                    w = v[0] | ((uint64_t)ab << kRingShift);
+                    // the path rules (they need no regions) here, off the audit waves' chains
+                    if (e.pid != spr.q) spr = puzzle_rules<1>(p, rt, e.pid);
+                    BB<1> vb;
+                    vb.w[0] = v[0];
+                    q_after = e.pid | (audit_path<1>(p.pitch, spr, vb, ab == spr.tbit) << kPidBits);
                 }
                 ring[at(b, j, col)] = w;
+                rpid[at(b, j, col)] = q_after;
                 trw[at(b, j, col)] = (uint8_t)code;
                 tfl[at(b, j, col)] = (uint8_t)f;
             }
@@ -1111,8 +1123,6 @@ __global__ void __launch_bounds__(64 * G * (1 + A))
 
     // ---- audit waves
     const uint32_t q = wv / (uint32_t)G - 1u;                    // audits the steps t % A == q
-    const uint32_t NP = p.tab.num_puzzles;
-    uint32_t pid = active ? p.st.pid[i] : 0u;
     PuzzleRules<1> pr;
     pr.q = 0xFFFFFFFFu;
     __syncthreads();                                             // B_0
@@ -1121,17 +1131,16 @@ __global__ void __launch_bounds__(64 * G * (1 + A))
         const int32_t kt = k - 1, cnt = tile_cnt(kt);
         const uint32_t b = (uint32_t)kt & 1u;
 #pragma unroll 1
-        for (int32_t j = 0; j < cnt; ++j) {
+        for (int32_t j = (int32_t)q; j < cnt; j += A) {          // this wave's steps of the tile
             const uint64_t w = ring[at(b, j, col)];
-            if (w >> 63) pid = pid + 1u == NP ? 0u : pid + 1u;   // an autoreset step: reset(), 1087
-            if ((uint32_t)j % (uint32_t)A != q) continue;        // another audit wave's step
+            const uint32_t pw = rpid[at(b, j, col)];
+            const uint32_t pid = pw & ((1u << kPidBits) - 1u);
             uint32_t out = 0;
             if (active) {
                 if (pid != pr.q) pr = puzzle_rules<1>(p, rt, pid);
                 BB<1> vb;
                 vb.w[0] = w & ((1ull << kRingShift) - 1ull);
-                const uint32_t ab = (uint32_t)(w >> kRingShift) & 63u;
-                out = audit_r<1, NoMemo, true>(p, rt, pr, vb, ab == pr.tbit, nullptr, nullptr).bits;
+                out = audit_r<1, NoMemo, true, true>(p, rt, pr, vb, false, nullptr, nullptr, 0, pw >> kPidBits).bits;
             }
             tbt[at(b, j, col)] = (uint16_t)out;
         }
@@ -1911,7 +1920,7 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
             }
         }
     }
-    c->ring_ok = W == 1;
+    c->ring_ok = W == 1 && t->num_puzzles < (1 << kPidBits);
     for (size_t q = 0; q < P; ++q)
         if ((t->info[4 * q] & 0xFFu) * pitch > kRingShift) c->ring_ok = false;
     c->num_puzzles = (uint32_t)t->num_puzzles;

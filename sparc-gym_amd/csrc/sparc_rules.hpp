@@ -516,6 +516,25 @@ __device__ __forceinline__ PuzzleRules<W> puzzle_rules(const Params& p, const Ru
     return r;
 }
 
+// The path rules of _run_rule_validators as their output bits: reached_target (487-495, bit 0),
+// path_not_crossing (497-505, bit 1: true by construction, a move only enters an unvisited point
+// and a pop removes the last one), no_gap_violations (507-517, bit 2), all_dots_collected (519-531,
+// bit 3) and triangles_edge_count (622-646, bit 6).  They read only the path and the puzzle's
+// planes (vis: path points, reached: the agent is on the target), not the regions.
+template <int W>
+__device__ __forceinline__ uint32_t audit_path(uint32_t P, const PuzzleRules<W>& pr, const BB<W>& vis, bool reached) {
+    // triangles: bit-sliced count of path neighbours (x±1: ±P, y±1: ±1)
+    const BB<W> a = vis.shr(P), b = vis.shl(P), c = vis.shr(1), d = vis.shl(1);
+    const BB<W> s1 = a ^ b, c1 = a & b, s2 = c ^ d, c2 = c & d;
+    const BB<W> n0 = s1 ^ s2, k0 = s1 & s2, n1 = c1 ^ c2 ^ k0, n2 = c1 & c2;
+    const BB<W> bad = pr.pl[kB_TRI] & ((n0 ^ pr.pl[kB_TRI0]) | (n1 ^ pr.pl[kB_TRI1]) | (n2 ^ pr.pl[kB_TRI2]));
+    const bool tri_ok = !bad.any();
+    const bool gap_ok = !(pr.pl[kB_GAPS] & vis).any();
+    const bool dot_ok = !pr.pl[kB_DOTS].andnot(vis).any();
+    return (uint32_t)reached | 2u | ((uint32_t)gap_ok << 2) | ((uint32_t)dot_ok << 3) | ((uint32_t)tri_ok << 6);
+}
+constexpr uint32_t kPathBits = 0x4Fu;   // the bits audit_path decides
+
 // vis: path points; reached: the agent is on the target (_rule_reached_target 487-495); pr: the
 // env's puzzle (puzzle_rules).  region_out (may be null): region id per bit.  memo (FitMemo, or
 // NoMemo): exact-fit answers carried between calls of one lane (puzzles without a region-code
@@ -524,9 +543,11 @@ __device__ __forceinline__ PuzzleRules<W> puzzle_rules(const Params& p, const Ru
 // of this audit's outputs, for the FitQueue entry of a search that passes the node cap (its
 // region then counts as passing and the bits carry SPARC_RULE_SEARCH_EXHAUSTED until the host has
 // finished the search; the region-code table never holds such a code after sparc_load_rules).
-template <int W, class Memo = NoMemo, bool TABLE_ONLY = false>
+// PATH_IN: the path rules' bits were computed elsewhere (audit_path) and come in as path_in.
+template <int W, class Memo = NoMemo, bool TABLE_ONLY = false, bool PATH_IN = false>
 __device__ RuleOut<W> audit_r(const Params& p, const RulesTab& rt, const PuzzleRules<W>& pr, const BB<W>& vis,
-                              bool reached, uint8_t* region_out, Memo* memo = nullptr, uint64_t pos = 0) {
+                              bool reached, uint8_t* region_out, Memo* memo = nullptr, uint64_t pos = 0,
+                              uint32_t path_in = 0) {
     const uint32_t q = pr.q, fo = pr.fo;
     const FitIn& fin = pr.fin;
     // the symbol planes only for a puzzle without a region-code table
@@ -610,17 +631,8 @@ __device__ RuleOut<W> audit_r(const Params& p, const RulesTab& rt, const PuzzleR
         ++rid;
     }
     if (tpend) take((tw >> tsh) & 15u, trid);
-    // triangles: bit-sliced count of path neighbours (x±1: ±P, y±1: ±1)
-    const BB<W> a = vis.shr(P), b = vis.shl(P), c = vis.shr(1), d = vis.shl(1);
-    const BB<W> s1 = a ^ b, c1 = a & b, s2 = c ^ d, c2 = c & d;
-    const BB<W> n0 = s1 ^ s2, k0 = s1 & s2, n1 = c1 ^ c2 ^ k0, n2 = c1 & c2;
-    const BB<W> bad = pr.pl[kB_TRI] & ((n0 ^ pr.pl[kB_TRI0]) | (n1 ^ pr.pl[kB_TRI1]) | (n2 ^ pr.pl[kB_TRI2]));
-    const bool tri_ok = !bad.any();
-    const bool gap_ok = !(gaps & vis).any();
-    const bool dot_ok = !pr.pl[kB_DOTS].andnot(vis).any();
-    uint32_t bits = (uint32_t)reached | 2u | ((uint32_t)gap_ok << 2) | ((uint32_t)dot_ok << 3) |
-                    ((uint32_t)sq_ok << 4) | ((uint32_t)star_ok << 5) | ((uint32_t)tri_ok << 6) |
-                    ((uint32_t)poly_ok << 7);
+    const uint32_t pb = PATH_IN ? path_in : audit_path<W>(P, pr, vis, reached);
+    uint32_t bits = pb | ((uint32_t)sq_ok << 4) | ((uint32_t)star_ok << 5) | ((uint32_t)poly_ok << 7);
     bits |= (uint32_t)((bits & 0xFFu) == 0xFFu) << 8;
     bits |= (uint32_t)exhausted << 9;
     return RuleOut<W>{bits, fit_ok};
