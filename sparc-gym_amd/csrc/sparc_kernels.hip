@@ -944,15 +944,17 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
 // computed twice and no audit wave carries step state.
 //   The step wave hands every env-step over as one u64 and one u32 in LDS rings: the visited
 // board (the bits below kRingShift: every W = 1 pool with x_size * pitch <= 57) | the agent's bit
-// << 57, and the puzzle index after the step | the path rules' bits << 24 (audit_path: reached,
-// gaps, dots, triangles need no regions, so the step wave, off the critical path, decides them).
-// An audit wave reads only its own steps and keeps the puzzle's rule row in registers while its
-// env stays on a puzzle.
+// << 57, and the puzzle index after the step.  An audit wave reads only its own steps and keeps
+// the puzzle's rule row in registers while its env stays on a puzzle.  The step wave is
+// pipelined as k_rollout1's env waves (the trie phase of step t-1 next to the move phase of step
+// t), and keeps the reset board of its env's puzzle for the visited plane, so its tile of steps
+// stays shorter than the audit waves' (MI355X: with the fused step and the path rules moved onto
+// it, it was the longer chain, 1,890 cycles per step against 840 per audit and audit wave).
 //   Per workgroup 64 * G envs = G step waves (0..G-1) + G * A audit waves (group g = wave % G);
 // tiles of RT steps, one barrier per tile.  In interval k the step waves step tile k and store
-// the rewards / flags of tile k-1 and the rule bits of tile k-2 (whole 16-B pieces of the
-// workgroup's rows), the audit waves audit tile k-1.  Only the step waves read and write the env
-// state.
+// the rewards / flags and the rule bits of tile k-2 (whole 16-B pieces of the workgroup's rows;
+// three reward / flag buffers, as tile k-1's last reward code is written in interval k), the
+// audit waves audit tile k-1.  Only the step waves read and write the env state.
 // Shape <G, A, RT>: G 64-env groups per workgroup, A audit waves per group (so G * (1 + A) waves
 // <= 16), RT steps per tile (a multiple of A).
 template <int G, int A, int RT>
@@ -962,18 +964,17 @@ struct R1Geom {
     static constexpr uint32_t kEnvs = 64u * G;                            // envs per workgroup (a tile row)
     static constexpr size_t kRing = 0;                                      // [2][RT][kEnvs] u64
     static constexpr size_t kPid = kRing + 2 * RT * kEnvs * 8;             // [2][RT][kEnvs] u32 puzzle index
-    static constexpr size_t kRew = kPid + 2 * RT * kEnvs * 4;              // [2][RT][kEnvs] reward codes
-    static constexpr size_t kFlg = kRew + 2 * RT * kEnvs;                  // [2][RT][kEnvs] flags
-    static constexpr size_t kBits = kFlg + 2 * RT * kEnvs;                 // [2][RT][kEnvs] u16 rule bits
+    static constexpr size_t kRew = kPid + 2 * RT * kEnvs * 4;              // [3][RT][kEnvs] reward codes
+    static constexpr size_t kFlg = kRew + 3 * RT * kEnvs;                  // [3][RT][kEnvs] flags
+    static constexpr size_t kBits = kFlg + 3 * RT * kEnvs;                 // [2][RT][kEnvs] u16 rule bits
     static constexpr size_t kAct = kBits + 2 * RT * kEnvs * 2;             // [G][RT][64] actions of the tile
     static constexpr size_t kStk = kAct + G * RT * 64;                     // [G][64 moves][64] move stacks
     static constexpr size_t kBase = kStk + (size_t)G * 64 * 64;            // then the W = 1 puzzle rows
 };
 constexpr uint32_t kRingShift = 57;
-constexpr uint32_t kPidBits = 24;   // the puzzle-index ring word: index | path-rule bits << 24
 
 template <bool TB, bool RAND, bool LDS_TABLE, int G, int A, int RT>
-__global__ void __launch_bounds__(64 * G * (1 + A))
+__global__ void __launch_bounds__(64 * G * (1 + A)) __attribute__((amdgpu_waves_per_eu(6)))
     k_rollout1r(Params p, int32_t T, const uint8_t* __restrict__ act, uint64_t seed, uint64_t t0,
                 int8_t* __restrict__ rew, uint8_t* __restrict__ flg, int4* __restrict__ stats, uint32_t tiled,
                 RulesTab rt, uint16_t* __restrict__ bits) {
@@ -1013,20 +1014,35 @@ __global__ void __launch_bounds__(64 * G * (1 + A))
         using Stack = typename std::conditional<TB, LdsStack<64>, RegStack>::type;
         Env<1, TB, Stack> e;
         if constexpr (TB) e.stk.col = smem + Geo::kStk + g * 4096u + lane;
-        if (active) e.load(p, src, i);
         int4 acc = make_int4(0, 0, 0, 0);
+        // the visited plane after a step is (free board at reset & ~free board now) | start: the
+        // reset board and start bit of the env's puzzle, kept from its last reset
+        uint64_t initc = 0;
+        uint32_t sbit = 0;
+        if (active) {
+            e.load(p, src, i);
+            // the step is pipelined as in k_rollout1: iteration t runs the trie phase of step
+            // t-1 next to the move phase of step t, so the trie-record gather of one step has a
+            // whole step to arrive; iteration 0's trie phase replays the stored step (its
+            // outputs are subtracted from the stats)
+            int c0;
+            uint32_t s0;
+            e.replay_outputs(c0, s0);
+            acc.x -= c0;
+            acc.z -= (int)s0;
+            initc = src.get_init(e.pid);
+            sbit = src.get_row1(e.pid).x & 0xFFu;
+        }
         const uint64_t gid = p.env_offset + i;
         uint8_t* ta = smem + Geo::kAct + g * (RT * 64u);
         const uint32_t r = lane >> 2, c = (lane & 3u) * 16u;    // this lane's 16-B piece of an action tile
         const bool tact = !RAND && full;                         // actions through the tile prefetch
-        PuzzleRules<1> spr;   // the env's puzzle rules, for the path rules this wave decides
-        spr.q = 0xFFFFFFFFu;
         u32x4 anext = {0u, 0u, 0u, 0u};
         if (tact && (int32_t)r < tile_cnt(0)) anext = nt_load16(act + (size_t)r * n + wg_base + g * 64u + c);
         // tile kt's rewards / flags, or rule bits, from LDS to HBM by the E step-wave lanes
-        auto store_rf = [&](int32_t kt) {
+        auto store_rf = [&](int32_t kt) {   // (reward / flag tiles: buffer kt % 3)
             const int32_t cnt = tile_cnt(kt);
-            const uint32_t b = (uint32_t)kt & 1u;
+            const uint32_t b = (uint32_t)kt % 3u;
             if (full) {
                 constexpr uint32_t kPer = E / 16u;               // 16-B pieces per row
                 for (uint32_t pi = col; pi < kPer * (uint32_t)cnt; pi += E) {
@@ -1076,37 +1092,52 @@ __global__ void __launch_bounds__(64 * G * (1 + A))
                 else if (tact) a = ta[j * 64 + (int32_t)lane];
                 else if (active) a = act[(size_t)t * n + i];
                 uint32_t f = 0;
-                int code = 0;
                 uint64_t w = 0;
                 uint32_t q_after = 0;
                 if (active) {
-                    code = e.advance(p, src, a, f);
+                    e.reset_next(p, src);                        // step t's autoreset: rows and board
+                    if (e.rs) {
+                        initc = e.fr;
+                        sbit = e.e;
+                    }
+                    const int code = e.phase_trie(p);            // step t-1
+                    f = e.phase_move(p, a);                      // step t
                     acc.x += code;
-                    acc.y += (int)e.pending;
                     acc.z += (int)e.solved;
-                    acc.w += (int)e.was_reset;
-                    uint64_t v[1];
-                    uint32_t ab;
-                    e.obs_words(p, src, v, ab);
-                    w = v[0] | ((uint64_t)ab << kRingShift);
-                    // the path rules (they need no regions) here, off the audit waves' chains
-                    if (e.pid != spr.q) spr = puzzle_rules<1>(p, rt, e.pid);
-                    BB<1> vb;
-                    vb.w[0] = v[0];
-                    q_after = e.pid | (audit_path<1>(p.pitch, spr, vb, ab == spr.tbit) << kPidBits);
+                    acc.y += (int)e.pending;
+                    acc.w += (int)e.s_rs;
+                    if (t > 0) {                                 // step t-1's reward code
+                        const int32_t tp = t - 1;
+                        trw[((uint32_t)(tp / RT) % 3u * (uint32_t)RT + (uint32_t)(tp % RT)) * E + col] = (uint8_t)code;
+                    }
+                    w = (((initc & ~e.fr) >> p.pitch) | (1ull << sbit)) | ((uint64_t)e.e << kRingShift);
+                    q_after = e.pid;
                 }
                 ring[at(b, j, col)] = w;
                 rpid[at(b, j, col)] = q_after;
-                trw[at(b, j, col)] = (uint8_t)code;
-                tfl[at(b, j, col)] = (uint8_t)f;
+                tfl[((uint32_t)k % 3u * (uint32_t)RT + (uint32_t)j) * E + col] = (uint8_t)f;
             }
-            if (k >= 1) store_rf(k - 1);
-            if (k >= 2) store_bits(k - 2);
+            // interval k stores the rewards / flags of tile k-2 (tile k-1's last reward code is
+            // written in this interval) and the rule bits of tile k-2 (audited in interval k-1)
+            if (k >= 2) {
+                store_rf(k - 2);
+                store_bits(k - 2);
+            }
             __syncthreads();                                     // B_{k+1}
         }
-        store_rf(K - 1);                                         // interval K: the last tile's audits run
-        if (K >= 2) store_bits(K - 2);
+        if (active) {                                            // the last step's trie phase
+            const int code = e.phase_trie(p);
+            acc.x += code;
+            acc.z += (int)e.solved;
+            const int32_t tp = T - 1;
+            trw[((uint32_t)(tp / RT) % 3u * (uint32_t)RT + (uint32_t)(tp % RT)) * E + col] = (uint8_t)code;
+        }
+        if (K >= 2) {                                            // interval K: the last tile's audits run
+            store_rf(K - 2);
+            store_bits(K - 2);
+        }
         __syncthreads();                                         // B_{K+1}
+        store_rf(K - 1);
         store_bits(K - 1);
         if (!active) return;
         e.store(p, src, i);
@@ -1133,14 +1164,14 @@ __global__ void __launch_bounds__(64 * G * (1 + A))
 #pragma unroll 1
         for (int32_t j = (int32_t)q; j < cnt; j += A) {          // this wave's steps of the tile
             const uint64_t w = ring[at(b, j, col)];
-            const uint32_t pw = rpid[at(b, j, col)];
-            const uint32_t pid = pw & ((1u << kPidBits) - 1u);
+            const uint32_t pid = rpid[at(b, j, col)];
             uint32_t out = 0;
             if (active) {
                 if (pid != pr.q) pr = puzzle_rules<1>(p, rt, pid);
                 BB<1> vb;
                 vb.w[0] = w & ((1ull << kRingShift) - 1ull);
-                out = audit_r<1, NoMemo, true, true>(p, rt, pr, vb, false, nullptr, nullptr, 0, pw >> kPidBits).bits;
+                const uint32_t ab = (uint32_t)(w >> kRingShift) & 63u;
+                out = audit_r<1, NoMemo, true>(p, rt, pr, vb, ab == pr.tbit, nullptr, nullptr).bits;
             }
             tbt[at(b, j, col)] = (uint16_t)out;
         }
@@ -1920,7 +1951,7 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
             }
         }
     }
-    c->ring_ok = W == 1 && t->num_puzzles < (1 << kPidBits);
+    c->ring_ok = W == 1;
     for (size_t q = 0; q < P; ++q)
         if ((t->info[4 * q] & 0xFFu) * pitch > kRingShift) c->ring_ok = false;
     c->num_puzzles = (uint32_t)t->num_puzzles;

@@ -39,6 +39,60 @@ VARIANTS = {
             __asm__ volatile("" ::: "memory");
             nx = trow[npid];
         }""")],
+    # k_rollout1r with s_memtime stamps (timing only: the stats buffer receives, per wave, role |
+    # total | barrier-wait | audit cycles at index N/2 + block * 16 + wave; tools/diag_r1r.py)
+    "stamps": [
+        ("sparc_kernels.hip", """        __syncthreads();                                         // B_0
+        for (int32_t k = 0; k < K; ++k) {
+            const int32_t cnt = tile_cnt(k);
+            const uint32_t b = (uint32_t)k & 1u;
+            if (tact) {""", """        uint64_t dg_bar = 0;
+        const uint64_t dg_t0 = __builtin_amdgcn_s_memtime();
+        __syncthreads();                                         // B_0
+        for (int32_t k = 0; k < K; ++k) {
+            const int32_t cnt = tile_cnt(k);
+            const uint32_t b = (uint32_t)k & 1u;
+            if (tact) {"""),
+        ("sparc_kernels.hip", """                store_bits(k - 2);
+            }
+            __syncthreads();                                     // B_{k+1}""", """                store_bits(k - 2);
+            }
+            { const uint64_t s0_ = __builtin_amdgcn_s_memtime(); __syncthreads(); dg_bar += __builtin_amdgcn_s_memtime() - s0_; }"""),
+        ("sparc_kernels.hip", """        store_bits(K - 1);
+        if (!active) return;
+        e.store(p, src, i);
+        if (stats) {""", """        store_bits(K - 1);
+        if (lane == 0 && stats) stats[p.n / 2 + blockIdx.x * 16 + wv] = make_int4(0, (int)(__builtin_amdgcn_s_memtime() - dg_t0), (int)dg_bar, 0);
+        if (!active) return;
+        e.store(p, src, i);
+        if (false) {"""),
+        ("sparc_kernels.hip", """    PuzzleRules<1> pr;
+    pr.q = 0xFFFFFFFFu;
+    __syncthreads();                                             // B_0
+    __syncthreads();                                             // B_1 (interval 0: no tile yet)""", """    PuzzleRules<1> pr;
+    pr.q = 0xFFFFFFFFu;
+    uint64_t dg_bar = 0, dg_aud = 0;
+    const uint64_t dg_t0 = __builtin_amdgcn_s_memtime();
+    __syncthreads();                                             // B_0
+    { const uint64_t s0_ = __builtin_amdgcn_s_memtime(); __syncthreads(); dg_bar += __builtin_amdgcn_s_memtime() - s0_; }"""),
+        ("sparc_kernels.hip", """            uint32_t out = 0;
+            if (active) {
+                if (pid != pr.q) pr = puzzle_rules<1>(p, rt, pid);""", """            uint32_t out = 0;
+            const uint64_t sa_ = __builtin_amdgcn_s_memtime();
+            if (active) {
+                if (pid != pr.q) pr = puzzle_rules<1>(p, rt, pid);"""),
+        ("sparc_kernels.hip", """            tbt[at(b, j, col)] = (uint16_t)out;
+        }
+        __syncthreads();                                         // B_{k+1}
+    }
+}""", """            tbt[at(b, j, col)] = (uint16_t)out;
+            dg_aud += __builtin_amdgcn_s_memtime() - sa_;
+        }
+        { const uint64_t s0_ = __builtin_amdgcn_s_memtime(); __syncthreads(); dg_bar += __builtin_amdgcn_s_memtime() - s0_; }
+    }
+    if (lane == 0 && stats) stats[p.n / 2 + blockIdx.x * 16 + wv] = make_int4((int)q + 1, (int)(__builtin_amdgcn_s_memtime() - dg_t0), (int)dg_bar, (int)dg_aud);
+}"""),
+    ],
 }
 
 
