@@ -973,6 +973,9 @@ struct R1Geom {
 };
 constexpr uint32_t kRingShift = 57;
 
+// amdgpu_waves_per_eu(6): two 12-wave workgroups per CU (3 waves per SIMD each).  Left to itself
+// the compiler takes 92 VGPRs (5 waves per SIMD, one workgroup per CU: 0.145 ms per 50-step launch
+// against 0.121 ms with 80 VGPRs and 24 B of scratch touched once per tile).
 template <bool TB, bool RAND, bool LDS_TABLE, int G, int A, int RT>
 __global__ void __launch_bounds__(64 * G * (1 + A)) __attribute__((amdgpu_waves_per_eu(6)))
     k_rollout1r(Params p, int32_t T, const uint8_t* __restrict__ act, uint64_t seed, uint64_t t0,

@@ -533,7 +533,6 @@ __device__ __forceinline__ uint32_t audit_path(uint32_t P, const PuzzleRules<W>&
     const bool dot_ok = !pr.pl[kB_DOTS].andnot(vis).any();
     return (uint32_t)reached | 2u | ((uint32_t)gap_ok << 2) | ((uint32_t)dot_ok << 3) | ((uint32_t)tri_ok << 6);
 }
-constexpr uint32_t kPathBits = 0x4Fu;   // the bits audit_path decides
 
 // vis: path points; reached: the agent is on the target (_rule_reached_target 487-495); pr: the
 // env's puzzle (puzzle_rules).  region_out (may be null): region id per bit.  memo (FitMemo, or
@@ -543,11 +542,9 @@ constexpr uint32_t kPathBits = 0x4Fu;   // the bits audit_path decides
 // of this audit's outputs, for the FitQueue entry of a search that passes the node cap (its
 // region then counts as passing and the bits carry SPARC_RULE_SEARCH_EXHAUSTED until the host has
 // finished the search; the region-code table never holds such a code after sparc_load_rules).
-// PATH_IN: the path rules' bits were computed elsewhere (audit_path) and come in as path_in.
-template <int W, class Memo = NoMemo, bool TABLE_ONLY = false, bool PATH_IN = false>
+template <int W, class Memo = NoMemo, bool TABLE_ONLY = false>
 __device__ RuleOut<W> audit_r(const Params& p, const RulesTab& rt, const PuzzleRules<W>& pr, const BB<W>& vis,
-                              bool reached, uint8_t* region_out, Memo* memo = nullptr, uint64_t pos = 0,
-                              uint32_t path_in = 0) {
+                              bool reached, uint8_t* region_out, Memo* memo = nullptr, uint64_t pos = 0) {
     const uint32_t q = pr.q, fo = pr.fo;
     const FitIn& fin = pr.fin;
     // the symbol planes only for a puzzle without a region-code table
@@ -631,7 +628,7 @@ __device__ RuleOut<W> audit_r(const Params& p, const RulesTab& rt, const PuzzleR
         ++rid;
     }
     if (tpend) take((tw >> tsh) & 15u, trid);
-    const uint32_t pb = PATH_IN ? path_in : audit_path<W>(P, pr, vis, reached);
+    const uint32_t pb = audit_path<W>(P, pr, vis, reached);
     uint32_t bits = pb | ((uint32_t)sq_ok << 4) | ((uint32_t)star_ok << 5) | ((uint32_t)poly_ok << 7);
     bits |= (uint32_t)((bits & 0xFFu) == 0xFFu) << 8;
     bits |= (uint32_t)exhausted << 9;
