@@ -39,6 +39,25 @@ VARIANTS = {
             __asm__ volatile("" ::: "memory");
             nx = trow[npid];
         }""")],
+    # c3 trie wave (TrieLane::step_core) without the reward code and counters: it hands over only
+    # the trie position class min(S >> 15, 2), the byte an I/O-wave reward stage would need (an
+    # upper bound on moving the reward selects off the trie wave; VERDICT r3 item 4, second item)
+    "notriecode": [("sparc_trie.hpp", """        const uint32_t x = S >> 15;                            // 0 on, 1 on a solution, >= 2 off
+        const int cd = x == 1u ? 100 : Oneg;
+        const int cm = moved ? (x < 2u ? hs : hsn) : 0;
+        const int code = done ? cd : cm;
+        Oneg = done ? (cd < 0 ? cd : 0) : -100;
+        acc_x += code;
+        acc_y += (uint32_t)done;
+        acc_z += (uint32_t)(code == 100);
+        return code;
+    }
+};""", """        const uint32_t x = S >> 15;
+        (void)moved;
+        (void)done;
+        return (int)(x < 2u ? x : 2u);
+    }
+};""")],
     # k_rollout1r with s_memtime stamps (timing only: the stats buffer receives, per wave, role |
     # total | barrier-wait | audit cycles at index N/2 + block * 16 + wave; tools/diag_r1r.py)
     "stamps": [
