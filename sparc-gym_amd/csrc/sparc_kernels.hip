@@ -726,7 +726,12 @@ constexpr size_t kS_FH = kS_Rew + kRing * 64;         // hand-over ring [64 step
 constexpr size_t kS_Stk = kS_FH + 4 * kRing * 64;     // move stack [64 moves][64]
 constexpr size_t kS_Pair = kS_Stk + 64 * 64;          // per move / trie wave pair
 constexpr size_t kS_Fin = 4 * kS_Pair;                // trie wave's final state [4][64] 2 x uint4
+// IOR: the final state is one uint4 per env (S, Oneg, pid) and the second half of the region holds
+// the per-env counters [3][256] int32 of the I/O waves (so that c3's 1,024 staged puzzle rows
+// still fit: 128 KB of tiles + 8 KB + 32 KB = 160 KB)
+constexpr size_t kS_Cnt = kS_Fin + 256 * sizeof(uint4);
 constexpr size_t kS_Base = kS_Fin + 4 * 64 * 2 * sizeof(uint4);
+static_assert(kS_Cnt + 3 * 256 * sizeof(int32_t) <= kS_Base, "k_rollout1s IOR counters");
 // LDS bytes of the staged rows: move rows + trie rows, 16 B each per puzzle
 __host__ __device__ constexpr size_t split_table_bytes(uint32_t P) { return (size_t)P * 2 * sizeof(uint4); }
 
@@ -746,7 +751,35 @@ __device__ __forceinline__ uint32_t flag_bytes4(const u32x4 w) {
     return lo | (hi << 16);
 }
 
-template <bool TB, bool RAND, bool LDS_TABLE, bool LA = false>
+// k_rollout1s<…, IOR> (next-step autoreset): the reward codes of four env-steps from their
+// hand-over words w, flag bytes F (flag_bytes4) and the trie wave's class bytes tb
+// (TrieLane::class_byte: class 0 on the trie, 1 on a solution, 2 off it, | hs << 2), four
+// bytes side by side (SWAR).  step() 1201-1223 with Oneg = -100 at every done step (a done step
+// is always followed by its autoreset step): done -> +100 on a solution else -100; moved ->
+// +hs on the trie, -hs off it; else 0.  Byte counters per env: done steps (cy), +100 steps (cz),
+// +1 steps (cp), -1 steps (cm); the episode reward sum is 200 cz - 100 cy + cp - cm.
+struct IoCounters {
+    uint32_t cy[4] = {0u, 0u, 0u, 0u}, cz[4] = {0u, 0u, 0u, 0u}, cp[4] = {0u, 0u, 0u, 0u}, cm[4] = {0u, 0u, 0u, 0u};
+};
+__device__ __forceinline__ uint32_t io_codes4(const u32x4 w, uint32_t F, uint32_t tb, uint32_t& cy, uint32_t& cz,
+                                              uint32_t& cp, uint32_t& cm) {
+    // byte 3 of each word: fwd - pop at bits 6-7 (bit 6 set iff the step moved, sparc_move1.hpp)
+    const uint32_t mv = __builtin_amdgcn_perm(w.y, w.x, 0x0C0C0703u) | (__builtin_amdgcn_perm(w.w, w.z, 0x0C0C0703u) << 16);
+    const uint32_t m1 = (mv >> 6) & 0x01010101u;
+    const uint32_t d1 = (F | (F >> 1)) & 0x01010101u;             // terminated | truncated
+    const uint32_t c2 = (tb >> 1) & 0x01010101u;                  // off the trie
+    const uint32_t c1 = tb & ~(tb >> 1) & 0x01010101u;            // on a solution
+    const uint32_t mh = m1 & (tb >> 2) & ~d1;                     // moved, not done, hs
+    const uint32_t pl = mh & ~c2, mi = mh & c2, dz = d1 & c1;
+    cy += d1;
+    cz += dz;
+    cp += pl;
+    cm += mi;
+    // selector 0: 0, 1: +1, 2: -1, 4: -100, 5: +100
+    return __builtin_amdgcn_perm(0x0000649Cu, 0x00FF0100u, pl | (mi << 1) | (d1 << 2) | dz);
+}
+
+template <bool TB, bool RAND, bool LDS_TABLE, bool LA = false, bool IOR = false>
 __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, const uint8_t* __restrict__ act,
                                                         uint64_t seed, uint64_t t0, int8_t* __restrict__ rew,
                                                         uint8_t* __restrict__ flg, int4* __restrict__ stats) {
@@ -778,6 +811,7 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         const uint32_t io = wv - 8u;
         const uint32_t r = lane >> 2, c = (lane & 3u) * 16u;
         const uint32_t pppp = p.pitch * 0x01010101u;
+        IoCounters ct;
         auto load_tile = [&](int32_t k) {                        // actions of tile k -> buffer k % 3
             if constexpr (!RAND) {
                 u32x4 v = nt_load16(act + (size_t)(k * kTile + r) * n + wg_base + io * 64 + c);
@@ -804,25 +838,68 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
             const uint32_t w = 2 * q + (c8 >> 6);
             const uint8_t* base = smem + w * kS_Pair + row * 64 + (c8 & 63u);
             const size_t o = (size_t)(k * kTile + h * 8 + r8) * n + wg_base + q * 128 + c8;
-            if (rew) nt_store16(reinterpret_cast<uint8_t*>(rew) + o, *reinterpret_cast<const u32x4*>(base + kS_Rew));
-            if (flg) {   // byte 0 of 16 hand-over words
-                const u32x4* fh = reinterpret_cast<const u32x4*>(smem + w * kS_Pair + kS_FH + row * 256 + 4 * (c8 & 63u));
-                u32x4 v;
-                v.x = flag_bytes4(fh[0]);
-                v.y = flag_bytes4(fh[1]);
-                v.z = flag_bytes4(fh[2]);
-                v.w = flag_bytes4(fh[3]);
-                nt_store16(flg + o, v);
+            const u32x4* fh = reinterpret_cast<const u32x4*>(smem + w * kS_Pair + kS_FH + row * 256 + 4 * (c8 & 63u));
+            if constexpr (IOR) {
+                // the reward codes from the class bytes and hand-over words (io_codes4)
+                const u32x4 tb = *reinterpret_cast<const u32x4*>(base + kS_Rew);
+                u32x4 f, v;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const u32x4 hw = fh[j];
+                    f[j] = flag_bytes4(hw);
+                    v[j] = io_codes4(hw, f[j], tb[j], ct.cy[j], ct.cz[j], ct.cp[j], ct.cm[j]);
+                }
+                if (rew) nt_store16(reinterpret_cast<uint8_t*>(rew) + o, v);
+                if (flg) nt_store16(flg + o, f);
+            } else {
+                if (rew) nt_store16(reinterpret_cast<uint8_t*>(rew) + o, *reinterpret_cast<const u32x4*>(base + kS_Rew));
+                if (flg) {   // byte 0 of 16 hand-over words
+                    u32x4 v;
+                    v.x = flag_bytes4(fh[0]);
+                    v.y = flag_bytes4(fh[1]);
+                    v.z = flag_bytes4(fh[2]);
+                    v.w = flag_bytes4(fh[3]);
+                    nt_store16(flg + o, v);
+                }
             }
         };
+        // IOR: the byte counters of this lane's 16 envs into the per-env LDS counters (reward sum,
+        // done steps, +100 steps), at least every 255 tiles (a lane counts one row per tile)
+        auto flush = [&]() {
+            const uint32_t col0 = (io & 1u) * 128u + (lane & 7u) * 16u;
+            int32_t* cnt = reinterpret_cast<int32_t*>(smem + kS_Cnt);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const uint32_t y = __builtin_amdgcn_ubfe(ct.cy[j], 8u * b, 8u), z = __builtin_amdgcn_ubfe(ct.cz[j], 8u * b, 8u);
+                    const int32_t pm = (int32_t)__builtin_amdgcn_ubfe(ct.cp[j], 8u * b, 8u) -
+                                       (int32_t)__builtin_amdgcn_ubfe(ct.cm[j], 8u * b, 8u);
+                    const uint32_t c = col0 + 4u * j + b;
+                    atomicAdd(cnt + c, 200 * (int32_t)z - 100 * (int32_t)y + pm);
+                    atomicAdd(cnt + 256 + c, (int32_t)y);
+                    atomicAdd(cnt + 512 + c, (int32_t)z);
+                }
+            }
+            ct = IoCounters{};
+        };
+        if constexpr (IOR) {
+            int32_t* cnt = reinterpret_cast<int32_t*>(smem + kS_Cnt);
+            for (uint32_t x = io * 64u + lane; x < 3u * 256u; x += 256u) cnt[x] = 0;
+        }
         if (K > 0) load_tile(0);
         __syncthreads();                                         // B_0
         for (int32_t k = 0; k <= K; ++k) {
             if (k + 1 < K) load_tile(k + 1);
-            if (k >= 2) store_tile(k - 2);
+            if (k >= 2) {
+                store_tile(k - 2);
+                if constexpr (IOR)
+                    if (((k - 2) & 127) == 127) flush();
+            }
             __syncthreads();                                     // B_{k+1}
         }
         if (K >= 1) store_tile(K - 1);
+        if constexpr (IOR) flush();
         __syncthreads();                                         // B_{K+2}
         return;
     }
@@ -830,7 +907,7 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
     const uint32_t pr = wv & 3u;                                 // the pair's 64 envs
     const uint32_t i = wg_base + pr * 64u + lane;
     uint8_t* pb = smem + pr * kS_Pair;
-    uint4* fin = reinterpret_cast<uint4*>(smem + kS_Fin) + 2u * (pr * 64u + lane);
+    uint4* fin = reinterpret_cast<uint4*>(smem + kS_Fin) + (IOR ? 1u : 2u) * (pr * 64u + lane);
     if (wv < 4) {                                                // ---- move waves
         MoveLane1<TB> m;
         uint8_t* col = pb + kS_Stk + lane;
@@ -871,8 +948,15 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         }
         __syncthreads();                                         // B_{K+1}
         __syncthreads();                                         // B_{K+2}: the trie state is in fin
-        const uint4 fs = fin[0];
-        const uint4 fc = fin[1];
+        uint4 fs = fin[0], fc;
+        if constexpr (IOR) {   // the counters from the I/O waves (io_codes4)
+            const int32_t* cnt = reinterpret_cast<const int32_t*>(smem + kS_Cnt) + pr * 64u + lane;
+            fc = make_uint4((uint32_t)cnt[256], fs.z, 0u, 0u);
+            fs.z = (uint32_t)cnt[0];
+            fs.w = (uint32_t)cnt[512];
+        } else {
+            fc = fin[1];
+        }
         const uint32_t pend = m.pending ? 1u : 0u;
         m.store(p, i, col, col_addr, fs.x, pend ? (fs.y == 0u ? 1u : 2u) : 0u, fc.y);
         if (stats) {
@@ -920,15 +1004,21 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     int code;
-                    if constexpr (LA) code = tl.step1la(hb[j], av[j], av[j + 1], trow, p.tab.trieg, NP);
-                    else code = tl.step1(hb[j], av[j], trow, p.tab.trie8, NP);
+                    if constexpr (LA) code = tl.step1la<!IOR>(hb[j], av[j], av[j + 1], trow, p.tab.trieg, NP);
+                    else code = tl.step1<!IOR>(hb[j], av[j], trow, p.tab.trie8, NP);
                     tr[(row0 + j) * 64] = (uint8_t)code;
                 }
             }
             __syncthreads();                                     // B_{k+1}
         }
-        fin[0] = make_uint4(tl.S, (uint32_t)tl.Oneg, (uint32_t)tl.acc_x, tl.acc_z);
-        fin[1] = make_uint4(tl.acc_y, tl.pid, 0u, 0u);
+        if constexpr (IOR)   // the last step's hand-over word is still in the ring
+            if (K > 0) tl.finish_oneg(th[((uint32_t)(K * kTile - 1) & (kRing - 1)) * 64u] & 0x30000u);
+        if constexpr (IOR) {
+            fin[0] = make_uint4(tl.S, (uint32_t)tl.Oneg, tl.pid, 0u);
+        } else {
+            fin[0] = make_uint4(tl.S, (uint32_t)tl.Oneg, (uint32_t)tl.acc_x, tl.acc_z);
+            fin[1] = make_uint4(tl.acc_y, tl.pid, 0u, 0u);
+        }
         __syncthreads();                                         // B_{K+2}
     }
 }
@@ -1435,6 +1525,7 @@ struct Ctx {
     bool r_tab_all = false;   // every puzzle has a region-code table (k_rollout1r's audit)
     bool ring_ok = false;     // W = 1 and every board fits below kRingShift (k_rollout1r's ring word)
     bool rules_generic = false;   // SPARC_RULE_ROLLOUT=generic: rule rollouts on k_rollout<..., RULES> (A/B, tests)
+    bool io_codes_off = false;    // SPARC_IO_CODES=off: k_rollout1s keeps the reward codes on the trie wave (A/B, tests)
     int r1r_shape = 0;            // SPARC_R1R_SHAPE: k_rollout1r's <G, A, RT> (0: <2, 5, 10>; 1, 2: A/B, tests)
     // exact-fit searches past the GPU's node cap (sparc_set_fit_cap) are finished on the host
     // from these copies of the rule table (sparc_rules.hpp exact_fit, the same code)
@@ -1634,6 +1725,7 @@ int sparc_create(int device, const sparc_config* cfg, void** ctx_out) {
     c->W = cfg->words;
     if (const char* v = getenv("SPARC_RULE_ROLLOUT")) c->rules_generic = strcmp(v, "generic") == 0;
     if (const char* v = getenv("SPARC_R1R_SHAPE")) c->r1r_shape = atoi(v);
+    if (const char* v = getenv("SPARC_IO_CODES")) c->io_codes_off = strcmp(v, "off") == 0;
     const size_t n = c->n;
     auto cleanup = [&](int code) {
         sparc_destroy(c);
@@ -2083,20 +2175,28 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
                 if (shm_s > 64 * 1024 && (lds_rc = allow_big_lds(c, reinterpret_cast<const void*>(kern)))) return;
                 kern<<<dim3((unsigned)blocks), kBlock1s, shm_s, c->stream>>>(p, T16, a, seed, t0, d_rew, d_flags, st);
             };
-            auto go_s = [&](auto tb) {
-                constexpr bool TB = decltype(tb)::value;
+            // IOR (next-step autoreset): the I/O waves derive the reward codes and counters from
+            // the trie wave's class bytes (io_codes4), which takes them off the trie wave's chain
+            auto go_s = [&](auto tb, auto ior) {
+                constexpr bool TB = decltype(tb)::value, IOR = decltype(ior)::value;
                 if (d_act) {
                     // look-ahead trie gathers on grids of at most 64 workgroups (sparc_trie.hpp)
-                    if (lds_s && blocks <= 64) launch_s(k_rollout1s<TB, false, true, true>, d_act);
-                    else if (lds_s) launch_s(k_rollout1s<TB, false, true>, d_act);
-                    else launch_s(k_rollout1s<TB, false, false>, d_act);
+                    if (lds_s && blocks <= 64) launch_s(k_rollout1s<TB, false, true, true, IOR>, d_act);
+                    else if (lds_s) launch_s(k_rollout1s<TB, false, true, false, IOR>, d_act);
+                    else launch_s(k_rollout1s<TB, false, false, false, IOR>, d_act);
                 } else {
-                    if (lds_s) launch_s(k_rollout1s<TB, true, true>, nullptr);
-                    else launch_s(k_rollout1s<TB, true, false>, nullptr);
+                    if (lds_s) launch_s(k_rollout1s<TB, true, true, false, IOR>, nullptr);
+                    else launch_s(k_rollout1s<TB, true, false, false, IOR>, nullptr);
                 }
             };
-            if (c->cfg.traceback) go_s(std::true_type{});
-            else go_s(std::false_type{});
+            const bool ior = p.autoreset == 1 && !c->io_codes_off;
+            if (c->cfg.traceback) {
+                if (ior) go_s(std::true_type{}, std::true_type{});
+                else go_s(std::true_type{}, std::false_type{});
+            } else {
+                if (ior) go_s(std::false_type{}, std::true_type{});
+                else go_s(std::false_type{}, std::false_type{});
+            }
             if (lds_rc) return lds_rc;
             rc = launch_check(c);
             if (rc || T16 == T) return rc;

@@ -40,6 +40,7 @@ struct TrieLane {
     uint32_t rx = ~0u, ry = ~0u;   // record of the current node (S & 0x7FFF)
     uint32_t base = 0, tmax = 0;
     int32_t hs = 0, hsn = 0;        // the puzzle has solutions (the +-1 rewards apply, 1217); -hs
+    uint32_t hsb = 0;               // hs << 2 (the class byte's bit 2, CODES = false)
     uint32_t pid = 0, npid = 0;
     uint4 nx;                       // trie row of npid, read at the previous reset
     int acc_x = 0;                  // sum of reward codes
@@ -60,6 +61,7 @@ struct TrieLane {
         tmax = r.w >> 17;
         hs = (int32_t)((r.w >> 14) & 1u);
         hsn = -hs;
+        hsb = (uint32_t)hs << 2;
         S = ((ps >> 24) << 16) | (ax & 0x7FFFu) | (((ax >> 19) & 1u) << 15);
         Oneg = ((ax >> 16) & 3u) == 1u ? 0 : -100;
         if ((r.w & 0x10000u) == 0u) {   // rootless puzzles keep off >= 1: the record is never read
@@ -83,6 +85,16 @@ struct TrieLane {
     // at most 64 workgroups.
     uint32_t nrx = ~0u, nry = ~0u;  // record of field[a] of the current node (a = this step's action)
 
+    // the class byte of a step (CODES = false): min(S >> 15, 2) (0 on the trie, 1 on a solution,
+    // 2 off it) | hs << 2.  With next-step autoreset the reward code is a function of this byte and
+    // the step's hand-over word alone (a done step never follows a done step, so Oneg is -100 at
+    // every done step), and the I/O wave computes it (io_codes4, k_rollout1s)
+    __device__ __forceinline__ uint32_t class_byte(uint32_t x) const { return (x < 2u ? x : 2u) | hsb; }
+    // Oneg after the launch's last step (CODES = false): 0 iff that step was done on a solution
+    __device__ __forceinline__ void finish_oneg(uint32_t last_hw_done) {
+        Oneg = (last_hw_done != 0u && (S >> 15) == 1u) ? 0 : -100;
+    }
+
     // after load(): the first step's look-ahead record (a0: its action)
     __device__ __forceinline__ void prime(const uint32_t a0, const uint2* __restrict__ trieg) {
         const uint32_t node = S & 0x7FFFu;
@@ -92,7 +104,7 @@ struct TrieLane {
     }
 
     // step1 (the W = 1 move wave's word) with the look-ahead record; an: the next step's action
-    template <class Rows>
+    template <bool CODES = true, class Rows>
     __device__ __forceinline__ int step1la(const uint32_t hw, const uint32_t a, const uint32_t an, const Rows& trow,
                                            const uint2* __restrict__ trieg, uint32_t num_puzzles) {
         const bool reset = (hw & 0x400000u) != 0u;
@@ -108,6 +120,7 @@ struct TrieLane {
             S = nx.w & 0x18000u;
             hs = (int32_t)((nx.w >> 14) & 1u);
             hsn = -hs;
+            hsb = (uint32_t)hs << 2;
             tmax = nx.w >> 17;
         }
         nx = trow[npid];
@@ -127,6 +140,7 @@ struct TrieLane {
         nrx = rec.x;
         nry = rec.y;
         const uint32_t x = S >> 15;
+        if constexpr (!CODES) return (int)class_byte(x);
         const int cd = x == 1u ? 100 : Oneg;
         const int cm = moved ? (x < 2u ? hs : hsn) : 0;
         const int code = done ? cd : cm;
@@ -147,16 +161,17 @@ struct TrieLane {
     }
     // the same from the W = 1 split move wave's word (sparc_move1.hpp): flag byte at bits 16-23,
     // fwd - pop at bits 30-31 (sign-extended down to bits 16-31)
-    template <class Rows>
+    template <bool CODES = true, class Rows>
     __device__ __forceinline__ int step1(const uint32_t hw, const uint32_t a, const Rows& trow,
                                          const uint2* __restrict__ trie8, uint32_t num_puzzles) {
-        return step_core((hw & 0x400000u) != 0u, (uint32_t)((int32_t)hw >> 14) & 0xFFFF0000u, hw >= 0x40000000u,
+        return step_core<CODES>((hw & 0x400000u) != 0u, (uint32_t)((int32_t)hw >> 14) & 0xFFFF0000u, hw >= 0x40000000u,
                          (hw & 0x30000u) != 0u, a, trow, trie8, num_puzzles);
     }
 
     // reset: an autoreset step; dd = (fwd - pop) << 16 (bit 16: moved); moved = dd != 0; done:
-    // terminated or truncated
-    template <class Rows>
+    // terminated or truncated.  CODES = false: the step returns the class byte instead of the
+    // reward code and keeps no counters (the I/O wave derives both, k_rollout1s<…, IOR>)
+    template <bool CODES = true, class Rows>
     __device__ __forceinline__ int step_core(const bool reset, const uint32_t dd, const bool moved, const bool done,
                                              const uint32_t a, const Rows& trow, const uint2* __restrict__ trie8,
                                              uint32_t num_puzzles) {
@@ -169,6 +184,7 @@ struct TrieLane {
             S = nx.w & 0x18000u;
             hs = (int32_t)((nx.w >> 14) & 1u);
             hsn = -hs;
+            hsb = (uint32_t)hs << 2;
             tmax = nx.w >> 17;
             // the row of the next reset, read here into the same registers, so nothing waits for
             // it until that reset (at least two steps later); the empty asm keeps the uses of the
@@ -198,6 +214,7 @@ struct TrieLane {
         // puzzle with solutions (on / off the trie), else 0 (an autoreset step neither moves
         // nor is done)
         const uint32_t x = S >> 15;                            // 0 on, 1 on a solution, >= 2 off
+        if constexpr (!CODES) return (int)class_byte(x);
         const int cd = x == 1u ? 100 : Oneg;
         const int cm = moved ? (x < 2u ? hs : hsn) : 0;
         const int code = done ? cd : cm;

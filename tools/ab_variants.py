@@ -5,7 +5,9 @@ applied (each `old` must occur exactly once), and the copy is built into ab/lib_
 product sources carry no diagnostic switches; variants that cut work give WRONG answers and exist
 only to locate time (never loaded by tests, smoke or bench).
 
-    python tools/ab_variants.py <variant> [<variant> ...]      (list: python tools/ab_variants.py)
+    python tools/ab_variants.py [--rev REV] <variant> [<variant> ...]   (list: python tools/ab_variants.py)
+
+--rev: the sources of git revision REV instead of the working tree (ab/lib_<variant>_<REV>.so).
 """
 import os
 import shutil
@@ -115,16 +117,22 @@ VARIANTS = {
 }
 
 
-def build(name, jobs_dir):
+def build(name, jobs_dir, rev=None):
     d = os.path.join(jobs_dir, name)
-    shutil.copytree(CSRC, d)
+    if rev:   # the sources of a git revision (e.g. the A/B baseline of uncommitted work)
+        os.makedirs(d)
+        arch = subprocess.run(["git", "-C", REPO, "archive", rev, "sparc-gym_amd/csrc"], check=True,
+                              capture_output=True).stdout
+        subprocess.run(["tar", "-x", "-C", d, "--strip-components=2"], input=arch, check=True)
+    else:
+        shutil.copytree(CSRC, d)
     for fname, old, new in VARIANTS[name]:
         path = os.path.join(d, fname)
         src = open(path).read()
         if src.count(old) != 1:
             raise SystemExit(f"variant {name}: {old!r} occurs {src.count(old)} times in {fname}")
         open(path, "w").write(src.replace(old, new))
-    out = os.path.join(REPO, "ab", f"lib_{name}.so")
+    out = os.path.join(REPO, "ab", f"lib_{name}{'_' + rev.replace('/', '_') if rev else ''}.so")
     os.makedirs(os.path.dirname(out), exist_ok=True)
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-I" + os.path.join(REPO, "include"), "-I" + d, "-o", out, os.path.join(d, "sparc_kernels.hip")]
@@ -133,11 +141,14 @@ def build(name, jobs_dir):
 
 def main():
     names = sys.argv[1:]
+    rev = None
+    if names[:1] == ["--rev"]:
+        rev, names = names[1], names[2:]
     if not names:
         print("variants:", ", ".join(VARIANTS))
         return
     with tempfile.TemporaryDirectory() as tmp:
-        procs = [build(n, tmp) for n in names]
+        procs = [build(n, tmp, rev) for n in names]
         rc = 0
         for p, out in procs:
             rc |= p.wait()
