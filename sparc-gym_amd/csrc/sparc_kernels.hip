@@ -761,11 +761,9 @@ __device__ __forceinline__ uint32_t flag_bytes4(const u32x4 w) {
 struct IoCounters {
     uint32_t cy[4] = {0u, 0u, 0u, 0u}, cz[4] = {0u, 0u, 0u, 0u}, cp[4] = {0u, 0u, 0u, 0u}, cm[4] = {0u, 0u, 0u, 0u};
 };
-__device__ __forceinline__ uint32_t io_codes4(const u32x4 w, uint32_t F, uint32_t tb, uint32_t& cy, uint32_t& cz,
-                                              uint32_t& cp, uint32_t& cm) {
-    // byte 3 of each word: fwd - pop at bits 6-7 (bit 6 set iff the step moved, sparc_move1.hpp)
-    const uint32_t mv = __builtin_amdgcn_perm(w.y, w.x, 0x0C0C0703u) | (__builtin_amdgcn_perm(w.w, w.z, 0x0C0C0703u) << 16);
-    const uint32_t m1 = (mv >> 6) & 0x01010101u;
+// m1: 0x01 in the bytes of the steps that moved
+__device__ __forceinline__ uint32_t io_codes4m(uint32_t m1, uint32_t F, uint32_t tb, uint32_t& cy, uint32_t& cz,
+                                               uint32_t& cp, uint32_t& cm) {
     const uint32_t d1 = (F | (F >> 1)) & 0x01010101u;             // terminated | truncated
     const uint32_t c2 = (tb >> 1) & 0x01010101u;                  // off the trie
     const uint32_t c1 = tb & ~(tb >> 1) & 0x01010101u;            // on a solution
@@ -777,6 +775,38 @@ __device__ __forceinline__ uint32_t io_codes4(const u32x4 w, uint32_t F, uint32_
     cm += mi;
     // selector 0: 0, 1: +1, 2: -1, 4: -100, 5: +100
     return __builtin_amdgcn_perm(0x0000649Cu, 0x00FF0100u, pl | (mi << 1) | (d1 << 2) | dz);
+}
+// the W = 1 hand-over words (sparc_move1.hpp): byte 3 holds fwd - pop at bits 6-7, bit 6 set iff
+// the step moved
+__device__ __forceinline__ uint32_t io_codes4(const u32x4 w, uint32_t F, uint32_t tb, uint32_t& cy, uint32_t& cz,
+                                              uint32_t& cp, uint32_t& cm) {
+    const uint32_t mv = __builtin_amdgcn_perm(w.y, w.x, 0x0C0C0703u) | (__builtin_amdgcn_perm(w.w, w.z, 0x0C0C0703u) << 16);
+    return io_codes4m((mv >> 6) & 0x01010101u, F, tb, cy, cz, cp, cm);
+}
+// the multi-word kernel's 16-bit words (hand_word16) of four env-steps, as two dwords lo, hi:
+// byte 0 the flag byte, byte 1 bits 0-1 fwd - pop + 1 (1: no move)
+__device__ __forceinline__ uint32_t io_codes4w(uint32_t lo, uint32_t hi, uint32_t F, uint32_t tb, uint32_t& cy,
+                                               uint32_t& cz, uint32_t& cp, uint32_t& cm) {
+    const uint32_t x = __builtin_amdgcn_perm(hi, lo, 0x07050301u) ^ 0x01010101u;   // 0 iff no move
+    return io_codes4m((x | (x >> 1)) & 0x01010101u, F, tb, cy, cz, cp, cm);
+}
+// the I/O wave's byte counters of its 16 envs (env columns col0 .. col0 + 15) into the per-env LDS
+// counters cnt[3][256] (reward sum, done steps, +100 steps)
+__device__ __forceinline__ void io_flush(IoCounters& ct, int32_t* cnt, uint32_t col0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const uint32_t y = __builtin_amdgcn_ubfe(ct.cy[j], 8u * b, 8u), z = __builtin_amdgcn_ubfe(ct.cz[j], 8u * b, 8u);
+            const int32_t pm = (int32_t)__builtin_amdgcn_ubfe(ct.cp[j], 8u * b, 8u) -
+                               (int32_t)__builtin_amdgcn_ubfe(ct.cm[j], 8u * b, 8u);
+            const uint32_t c = col0 + 4u * j + b;
+            atomicAdd(cnt + c, 200 * (int32_t)z - 100 * (int32_t)y + pm);
+            atomicAdd(cnt + 256 + c, (int32_t)y);
+            atomicAdd(cnt + 512 + c, (int32_t)z);
+        }
+    }
+    ct = IoCounters{};
 }
 
 template <bool TB, bool RAND, bool LDS_TABLE, bool LA = false, bool IOR = false>
@@ -865,23 +895,8 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         };
         // IOR: the byte counters of this lane's 16 envs into the per-env LDS counters (reward sum,
         // done steps, +100 steps), at least every 255 tiles (a lane counts one row per tile)
-        auto flush = [&]() {
-            const uint32_t col0 = (io & 1u) * 128u + (lane & 7u) * 16u;
-            int32_t* cnt = reinterpret_cast<int32_t*>(smem + kS_Cnt);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    const uint32_t y = __builtin_amdgcn_ubfe(ct.cy[j], 8u * b, 8u), z = __builtin_amdgcn_ubfe(ct.cz[j], 8u * b, 8u);
-                    const int32_t pm = (int32_t)__builtin_amdgcn_ubfe(ct.cp[j], 8u * b, 8u) -
-                                       (int32_t)__builtin_amdgcn_ubfe(ct.cm[j], 8u * b, 8u);
-                    const uint32_t c = col0 + 4u * j + b;
-                    atomicAdd(cnt + c, 200 * (int32_t)z - 100 * (int32_t)y + pm);
-                    atomicAdd(cnt + 256 + c, (int32_t)y);
-                    atomicAdd(cnt + 512 + c, (int32_t)z);
-                }
-            }
-            ct = IoCounters{};
+        auto flush_counts = [&]() {
+            io_flush(ct, reinterpret_cast<int32_t*>(smem + kS_Cnt), (io & 1u) * 128u + (lane & 7u) * 16u);
         };
         if constexpr (IOR) {
             int32_t* cnt = reinterpret_cast<int32_t*>(smem + kS_Cnt);
@@ -894,12 +909,12 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
             if (k >= 2) {
                 store_tile(k - 2);
                 if constexpr (IOR)
-                    if (((k - 2) & 127) == 127) flush();
+                    if (((k - 2) & 127) == 127) flush_counts();
             }
             __syncthreads();                                     // B_{k+1}
         }
         if (K >= 1) store_tile(K - 1);
-        if constexpr (IOR) flush();
+        if constexpr (IOR) flush_counts();
         __syncthreads();                                         // B_{K+2}
         return;
     }
@@ -1283,7 +1298,7 @@ __global__ void __launch_bounds__(64 * G * (1 + A)) __attribute__((amdgpu_waves_
 constexpr size_t kW_Act = 0, kW_Rew = 2 * kTile * 64, kW_Hand = kW_Rew + kRing * 64, kW_Board = kW_Hand + 2 * kRing * 64;
 __host__ __device__ constexpr size_t splitw_fin_bytes() { return 4 * 64 * 2 * sizeof(uint4); }
 
-template <int W, bool TB, bool RAND, bool LDS_TABLE>
+template <int W, bool TB, bool RAND, bool LDS_TABLE, bool IOR = false>
 __global__ void __launch_bounds__(kBlock1s) k_rolloutWs(Params p, SplitGeom g, const uint4* __restrict__ mrow,
                                                         const uint32_t* __restrict__ boards, int32_t T,
                                                         const uint8_t* __restrict__ act, uint64_t seed, uint64_t t0,
@@ -1304,9 +1319,12 @@ __global__ void __launch_bounds__(kBlock1s) k_rolloutWs(Params p, SplitGeom g, c
     const uint32_t wg_base = blockIdx.x * 256u;
     const int32_t K = T / kTile;
 
+    // IOR (as k_rollout1s): the final state one uint4 per env, the counters in the second half
+    int32_t* const cnt = reinterpret_cast<int32_t*>(smem + fin_off + 256 * sizeof(uint4));
     if (wv >= 8) {                                               // ---- the I/O waves (as k_rollout1s)
         const uint32_t io = wv - 8u;
         const uint32_t r = lane >> 2, c = (lane & 3u) * 16u;
+        IoCounters ct;
         auto load_tile = [&](int32_t k) {
             if constexpr (!RAND) {
                 const u32x4 v = nt_load16(act + (size_t)(k * kTile + r) * n + wg_base + io * 64 + c);
@@ -1320,26 +1338,49 @@ __global__ void __launch_bounds__(kBlock1s) k_rolloutWs(Params p, SplitGeom g, c
             const uint32_t w = 2 * q + (c8 >> 6);
             const uint8_t* base = smem + w * g.pair + row * 64 + (c8 & 63u);
             const size_t o = (size_t)(k * kTile + h * 8 + r8) * n + wg_base + q * 128 + c8;
-            if (rew) nt_store16(reinterpret_cast<uint8_t*>(rew) + o, *reinterpret_cast<const u32x4*>(base + kW_Rew));
-            if (flg) {   // byte 0 of 16 u16 hand-over words
-                const u32x4* fh = reinterpret_cast<const u32x4*>(smem + w * g.pair + kW_Hand + row * 128 + 2 * (c8 & 63u));
+            const u32x4* fh = reinterpret_cast<const u32x4*>(smem + w * g.pair + kW_Hand + row * 128 + 2 * (c8 & 63u));
+            if constexpr (IOR) {
                 const u32x4 a = fh[0], b = fh[1];
-                u32x4 v;
-                v.x = __builtin_amdgcn_perm(a.y, a.x, 0x06040200u);
-                v.y = __builtin_amdgcn_perm(a.w, a.z, 0x06040200u);
-                v.z = __builtin_amdgcn_perm(b.y, b.x, 0x06040200u);
-                v.w = __builtin_amdgcn_perm(b.w, b.z, 0x06040200u);
-                nt_store16(flg + o, v);
+                const u32x4 tb = *reinterpret_cast<const u32x4*>(base + kW_Rew);
+                u32x4 f, v;
+                f.x = __builtin_amdgcn_perm(a.y, a.x, 0x06040200u);
+                f.y = __builtin_amdgcn_perm(a.w, a.z, 0x06040200u);
+                f.z = __builtin_amdgcn_perm(b.y, b.x, 0x06040200u);
+                f.w = __builtin_amdgcn_perm(b.w, b.z, 0x06040200u);
+                v.x = io_codes4w(a.x, a.y, f.x, tb.x, ct.cy[0], ct.cz[0], ct.cp[0], ct.cm[0]);
+                v.y = io_codes4w(a.z, a.w, f.y, tb.y, ct.cy[1], ct.cz[1], ct.cp[1], ct.cm[1]);
+                v.z = io_codes4w(b.x, b.y, f.z, tb.z, ct.cy[2], ct.cz[2], ct.cp[2], ct.cm[2]);
+                v.w = io_codes4w(b.z, b.w, f.w, tb.w, ct.cy[3], ct.cz[3], ct.cp[3], ct.cm[3]);
+                if (rew) nt_store16(reinterpret_cast<uint8_t*>(rew) + o, v);
+                if (flg) nt_store16(flg + o, f);
+            } else {
+                if (rew) nt_store16(reinterpret_cast<uint8_t*>(rew) + o, *reinterpret_cast<const u32x4*>(base + kW_Rew));
+                if (flg) {   // byte 0 of 16 u16 hand-over words
+                    const u32x4 a = fh[0], b = fh[1];
+                    u32x4 v;
+                    v.x = __builtin_amdgcn_perm(a.y, a.x, 0x06040200u);
+                    v.y = __builtin_amdgcn_perm(a.w, a.z, 0x06040200u);
+                    v.z = __builtin_amdgcn_perm(b.y, b.x, 0x06040200u);
+                    v.w = __builtin_amdgcn_perm(b.w, b.z, 0x06040200u);
+                    nt_store16(flg + o, v);
+                }
             }
         };
+        if constexpr (IOR)
+            for (uint32_t x = io * 64u + lane; x < 3u * 256u; x += 256u) cnt[x] = 0;
         if (K > 0) load_tile(0);
         __syncthreads();                                         // B_0
         for (int32_t k = 0; k <= K; ++k) {
             if (k + 1 < K) load_tile(k + 1);
-            if (k >= 2) store_tile(k - 2);
+            if (k >= 2) {
+                store_tile(k - 2);
+                if constexpr (IOR)
+                    if (((k - 2) & 127) == 127) io_flush(ct, cnt, (io & 1u) * 128u + (lane & 7u) * 16u);
+            }
             __syncthreads();                                     // B_{k+1}
         }
         if (K >= 1) store_tile(K - 1);
+        if constexpr (IOR) io_flush(ct, cnt, (io & 1u) * 128u + (lane & 7u) * 16u);
         __syncthreads();                                         // B_{K+2}
         return;
     }
@@ -1347,7 +1388,7 @@ __global__ void __launch_bounds__(kBlock1s) k_rolloutWs(Params p, SplitGeom g, c
     const uint32_t pr = wv & 3u;
     const uint32_t i = wg_base + pr * 64u + lane;
     uint8_t* pb = smem + pr * g.pair;
-    uint4* fin = reinterpret_cast<uint4*>(smem + fin_off) + 2u * (pr * 64u + lane);
+    uint4* fin = reinterpret_cast<uint4*>(smem + fin_off) + (IOR ? 1u : 2u) * (pr * 64u + lane);
     if (wv < 4) {                                                // ---- move waves
         MoveLaneW<TB> m;
         m.bd = reinterpret_cast<uint32_t*>(pb + g.off_board) + lane;
@@ -1378,8 +1419,15 @@ __global__ void __launch_bounds__(kBlock1s) k_rolloutWs(Params p, SplitGeom g, c
         }
         __syncthreads();                                         // B_{K+1}
         __syncthreads();                                         // B_{K+2}: the trie state is in fin
-        const uint4 fs = fin[0];
-        const uint4 fc = fin[1];
+        uint4 fs = fin[0], fc;
+        if constexpr (IOR) {   // the counters from the I/O waves (io_codes4w)
+            const uint32_t col = pr * 64u + lane;
+            fc = make_uint4((uint32_t)cnt[256 + col], 0u, 0u, 0u);
+            fs.z = (uint32_t)cnt[col];
+            fs.w = (uint32_t)cnt[512 + col];
+        } else {
+            fc = fin[1];
+        }
         m.template store<W>(p, g, i, fs.x, m.pending ? (fs.y == 0u ? 1u : 2u) : 0u);
         if (stats) {
             const uint32_t resets = p.autoreset == 1 ? pend0 + fc.x - m.pending : 0u;
@@ -1409,13 +1457,18 @@ __global__ void __launch_bounds__(kBlock1s) k_rolloutWs(Params p, SplitGeom g, c
                 for (int j = 0; j < 4; ++j) hb[j] = th[(row0 + j) * 64];
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
-                    tr[(row0 + j) * 64] = (uint8_t)tl.step(widen_hand_word(hb[j]), __builtin_amdgcn_ubfe(hb[j], 10u, 2u),
-                                                           trow, p.tab.trie8, NP);
+                    tr[(row0 + j) * 64] = (uint8_t)tl.step<!IOR>(widen_hand_word(hb[j]), __builtin_amdgcn_ubfe(hb[j], 10u, 2u),
+                                                                 trow, p.tab.trie8, NP);
             }
             __syncthreads();                                     // B_{k+1}
         }
-        fin[0] = make_uint4(tl.S, (uint32_t)tl.Oneg, (uint32_t)tl.acc_x, tl.acc_z);
-        fin[1] = make_uint4(tl.acc_y, 0u, 0u, 0u);
+        if constexpr (IOR) {   // the last step's hand-over word is still in the ring
+            if (K > 0) tl.finish_oneg(th[((uint32_t)(K * kTile - 1) & (kRing - 1)) * 64u] & 3u);
+            fin[0] = make_uint4(tl.S, (uint32_t)tl.Oneg, 0u, 0u);
+        } else {
+            fin[0] = make_uint4(tl.S, (uint32_t)tl.Oneg, (uint32_t)tl.acc_x, tl.acc_z);
+            fin[1] = make_uint4(tl.acc_y, 0u, 0u, 0u);
+        }
         __syncthreads();                                         // B_{K+2}
     }
 }
@@ -2287,13 +2340,19 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
                     kern<<<dim3((unsigned)blocks), kBlock1s, shm, c->stream>>>(p, g, c->t_mroww, c->t_boardw, T16, a, seed,
                                                                               t0, d_rew, d_flags, st);
                 };
-                if (d_act) {
-                    if (lds_t) launch(k_rolloutWs<W, TB, false, true>, d_act);
-                    else launch(k_rolloutWs<W, TB, false, false>, d_act);
-                } else {
-                    if (lds_t) launch(k_rolloutWs<W, TB, true, true>, nullptr);
-                    else launch(k_rolloutWs<W, TB, true, false>, nullptr);
-                }
+                auto go = [&](auto ior) {
+                    constexpr bool IOR = decltype(ior)::value;
+                    if (d_act) {
+                        if (lds_t) launch(k_rolloutWs<W, TB, false, true, IOR>, d_act);
+                        else launch(k_rolloutWs<W, TB, false, false, IOR>, d_act);
+                    } else {
+                        if (lds_t) launch(k_rolloutWs<W, TB, true, true, IOR>, nullptr);
+                        else launch(k_rolloutWs<W, TB, true, false, IOR>, nullptr);
+                    }
+                };
+                // IOR (next-step autoreset): reward codes and counters on the I/O waves (k_rollout1s)
+                if (p.autoreset == 1 && !c->io_codes_off) go(std::true_type{});
+                else go(std::false_type{});
             }
         });
         if (lds_rc) return lds_rc;

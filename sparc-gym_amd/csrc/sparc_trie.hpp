@@ -153,10 +153,10 @@ struct TrieLane {
 
     // one env-step from its hand-over word (layout above) and action; returns the reward code
     // (x100, 1201-1223)
-    template <class Rows>
+    template <bool CODES = true, class Rows>
     __device__ __forceinline__ int step(const uint32_t hw, const uint32_t a, const Rows& trow,
                                         const uint2* __restrict__ trie8, uint32_t num_puzzles) {
-        return step_core((hw & 0x40u) != 0u, hw & 0xFFFF0000u, hw >= 0x10000u, (hw & 3u) != 0u, a, trow, trie8,
+        return step_core<CODES>((hw & 0x40u) != 0u, hw & 0xFFFF0000u, hw >= 0x10000u, (hw & 3u) != 0u, a, trow, trie8,
                          num_puzzles);
     }
     // the same from the W = 1 split move wave's word (sparc_move1.hpp): flag byte at bits 16-23,

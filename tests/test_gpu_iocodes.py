@@ -3,6 +3,8 @@ default under next-step autoreset): the trie wave hands over a class byte per en
 I/O waves compute the codes four envs per dword (io_codes4) and count per env in bytes, flushed
 to LDS at least every 128 tiles.  Checked bit-exact against the C oracle:
 
+* the W = 1 kernel and the multi-word kernel (k_rolloutWs<4>, k_rolloutWs<2>: 16-bit words,
+  io_codes4w);
 * many 16-step launches (every launch end is a chance for a done last step: the stored
   outcome, i.e. Oneg after the launch, comes from TrieLane::finish_oneg), with and without
   traceback, so that both solved and failed done steps end launches;
@@ -23,8 +25,12 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-def _pool():
-    proc = process_puzzles(synthetic.make_puzzles(1024, seed=0, sizes=((3, 3),), full_properties=True))
+# W = 1 (k_rollout1s), 15 x 15 points (k_rolloutWs<4>), mixed 5 x 5 - 11 x 11 (k_rolloutWs<2>)
+POOLS = {"w1": ((3, 3),), "w4": ((7, 7),), "mixed": ((2, 2), (3, 3), (4, 4), (5, 5))}
+
+
+def _pool(sizes):
+    proc = process_puzzles(synthetic.make_puzzles(1024, seed=0, sizes=sizes, full_properties=True))
     opool = [{"x_size": p["x_size"], "y_size": p["y_size"], "start": list(p["start_location"]),
               "target": list(p["target_location"]), "solution_count": p["solution_count"],
               "solution_paths": p["solution_paths"], "gaps": p["obs_array"]["gaps"]} for p in proc]
@@ -46,9 +52,9 @@ def _ostate(o):
             "outcome": s["outcome"]}
 
 
-def _run(tb, launches, T, io_off):
+def _run(pool, tb, launches, T, io_off):
     from sparc_gym_amd import SPaRCVecEnv
-    proc, table, opool = _pool()
+    proc, table, opool = _pool(POOLS[pool])
     n = 1024
     old = os.environ.get("SPARC_IO_CODES")
     if io_off:
@@ -74,9 +80,10 @@ def _run(tb, launches, T, io_off):
     return outs, opool
 
 
+@pytest.mark.parametrize("pool", list(POOLS))
 @pytest.mark.parametrize("tb", [True, False])
-def test_io_codes_short_launches_vs_oracle(on_gpu, tb):
-    outs, opool = _run(tb, 48, 16, False)
+def test_io_codes_short_launches_vs_oracle(on_gpu, pool, tb):
+    outs, opool = _run(pool, tb, 48, 16, False)
     n = 1024
     o = COracle(opool, n, tb, 2000, autoreset=1)
     o.reset(_pids(n))
@@ -92,17 +99,19 @@ def test_io_codes_short_launches_vs_oracle(on_gpu, tb):
         for k in ends:
             ends[k] += int((so["outcome"] == k).sum())
     # launches did end on solved and on failed done steps (outcome 1 / -1 in the stored state)
-    assert ends[1] > 0 and ends[-1] > 0, ends
+    # (15 x 15 with traceback: random walks rarely solve, ~1 launch end in 48)
+    assert ends[-1] > 0 and (ends[1] > 0 or (pool == "w4" and tb)), ends
     # and the trie-wave path gives the same outputs
-    outs_off, _ = _run(tb, 48, 16, True)
+    outs_off, _ = _run(pool, tb, 48, 16, True)
     for a, b in zip(outs, outs_off):
         for x, y in zip(a[1:3] + (a[4],), b[1:3] + (b[4],)):
             assert np.array_equal(x, y)
 
 
-def test_io_codes_long_launch_flushes_vs_oracle(on_gpu):
+@pytest.mark.parametrize("pool", ["w1", "w4"])
+def test_io_codes_long_launch_flushes_vs_oracle(on_gpu, pool):
     T = 4160   # 260 tiles: the byte counters flush after tiles 127 and 255 and at the end
-    outs, opool = _run(True, 1, T, False)
+    outs, opool = _run(pool, True, 1, T, False)
     acts, r, f, s, st = outs[0]
     n = 1024
     o = COracle(opool, n, True, 2000, autoreset=1)

@@ -60,6 +60,16 @@ VARIANTS = {
         return (int)(x < 2u ? x : 2u);
     }
 };""")],
+    # the W = 1 flood fill with the -y runs filled in one step too: the +y carry fill applied to the
+    # bit-reversed board (v_bfrev_b32 per half), instead of one -y step per iteration
+    "downfill": [("sparc_rules.hpp", """                const uint64_t up = (((a + r) ^ a) & a) | r;
+                N.w[0] = up | (r >> 1) | (r << P) | (r >> P);""", """                const uint64_t up = (((a + r) ^ a) & a) | r;
+                auto rev64 = [](uint64_t x) {
+                    return ((uint64_t)__builtin_bitreverse32((uint32_t)x) << 32) | __builtin_bitreverse32((uint32_t)(x >> 32));
+                };
+                const uint64_t ra = rev64(a), rr = rev64(r);
+                const uint64_t dn = rev64((((ra + rr) ^ ra) & ra) | rr);
+                N.w[0] = up | dn | (r << P) | (r >> P);""")],
     # k_rollout1r with s_memtime stamps (timing only: the stats buffer receives, per wave, role |
     # total | barrier-wait | audit cycles at index N/2 + block * 16 + wave; tools/diag_r1r.py)
     "stamps": [

@@ -14,10 +14,12 @@ __device__ __forceinline__ uint64_t stamp() { return __builtin_amdgcn_s_memtime(
 template <int G>
 struct DiagTrieLane : TrieLane {
     const uint4* lds_rows = nullptr;
-    template <class Rows>
+    // CODES = false (IOR): the product's class byte for G == 0; the timing-only gather variants
+    // (G != 0) keep their reward codes
+    template <bool CODES = true, class Rows>
     __device__ __forceinline__ int step1d(const uint32_t hw, const uint32_t a, const Rows& trow,
                                           const uint2* __restrict__ trie8, uint32_t num_puzzles) {
-        if constexpr (G == 0) return step1(hw, a, trow, trie8, num_puzzles);
+        if constexpr (G == 0) return step1<CODES>(hw, a, trow, trie8, num_puzzles);
         const bool reset = (hw & 0x400000u) != 0u;
         const uint32_t dd = (uint32_t)((int32_t)hw >> 14) & 0xFFFF0000u;
         const bool moved = hw >= 0x40000000u, done = (hw & 0x30000u) != 0u;
@@ -157,6 +159,8 @@ extern "C" int sparc_diag_rollout1s(void* ctx, int32_t T, const uint8_t* d_act, 
         kern<<<dim3(c->n / 256), kBlock1s, shm, c->stream>>>(p, T, d_act, 0, 0, d_rew, d_flags,
                                                             reinterpret_cast<int4*>(d_stats), d_times);
     };
+    // the product's I/O-wave reward codes (IOR: next-step autoreset, the bench configs)
+    if (p.autoreset != 1) return fail(c, SPARC_E_INVALID, "diag: needs next-step autoreset (IOR)");
     // variant % 10: the trie wave's record gather, 0 = global (the product's), 1 = LDS, 2 = none;
     // variant / 10: the move wave's autoreset (DiagMoveLane1)
     const int g = variant % 10, mv = variant / 10;
@@ -164,10 +168,10 @@ extern "C" int sparc_diag_rollout1s(void* ctx, int32_t T, const uint8_t* d_act, 
         constexpr bool TB = decltype(tb)::value;
         auto pg = [&](auto mvc) {
             constexpr int MV = decltype(mvc)::value;
-            if (g == 1) go(k_rollout1s_diag<TB, false, true, 1, MV>);
-            else if (g == 2) go(k_rollout1s_diag<TB, false, true, 2, MV>);
-            else if (g == 3) go(k_rollout1s_diag<TB, false, true, 3, MV>);
-            else go(k_rollout1s_diag<TB, false, true, 0, MV>);
+            if (g == 1) go(k_rollout1s_diag<TB, false, true, 1, MV, false, true>);
+            else if (g == 2) go(k_rollout1s_diag<TB, false, true, 2, MV, false, true>);
+            else if (g == 3) go(k_rollout1s_diag<TB, false, true, 3, MV, false, true>);
+            else go(k_rollout1s_diag<TB, false, true, 0, MV, false, true>);
         };
         if (mv == 1) pg(std::integral_constant<int, 1>{});
         else if (mv == 2) pg(std::integral_constant<int, 2>{});
