@@ -102,6 +102,9 @@ struct MoveLane1 {
             }
             step = -1;   // this step's increment brings it to 0
             lv = kHwReset;
+            // keep the uses of the old row above the read (as TrieLane::step_core): without this
+            // the compiler issued the read first into temporaries and waited for it in the branch
+            __asm__ volatile("" ::"v"(fr), "v"(e), "v"(tgt), "v"(pflags) : "memory");
             rr = mrow[rr.w];
         }
     }

@@ -70,6 +70,11 @@ VARIANTS = {
                 const uint64_t ra = rev64(a), rr = rev64(r);
                 const uint64_t dn = rev64((((ra + rr) ^ ra) & ra) | rr);
                 N.w[0] = up | dn | (r << P) | (r >> P);""")],
+    # the observation planes stored with the default cache policy instead of nontemporal
+    "obswb": [("sparc_kernels.hip", """            if (vout) __builtin_nontemporal_store(u32x4{vv[0], vv[1], vv[2], vv[3]}, reinterpret_cast<u32x4*>(vout + f));
+            if (aout) __builtin_nontemporal_store(u32x4{aa[0], aa[1], aa[2], aa[3]}, reinterpret_cast<u32x4*>(aout + f));""",
+               """            if (vout) *reinterpret_cast<u32x4*>(vout + f) = u32x4{vv[0], vv[1], vv[2], vv[3]};
+            if (aout) *reinterpret_cast<u32x4*>(aout + f) = u32x4{aa[0], aa[1], aa[2], aa[3]};""")],
     # k_rollout1r with s_memtime stamps (timing only: the stats buffer receives, per wave, role |
     # total | barrier-wait | audit cycles at index N/2 + block * 16 + wave; tools/diag_r1r.py)
     "stamps": [
