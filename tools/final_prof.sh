@@ -13,6 +13,6 @@ for spec in ${PROF_SPECS:-"c3:65536:2000:k_rollout1s" "c2:4096:2000:k_rollout1s"
   IFS=: read cfg envs chunk kern <<< "$spec"
   step prof_$cfg 420 bash tools/collect_profiles.sh gpurun_out/prof_$cfg $cfg $envs $chunk 5
   d=gpurun_out/prof_$cfg
-  step fold_$cfg 60 python tools/pmc_traffic.py ${cfg}_rollout_n${envs}_chunk${chunk} $kern $d/pmc_fetch.csv $d/pmc_write.csv $d/pmc_sq1.csv $d/pmc_sq2.csv
+  step fold_$cfg 60 python tools/pmc_traffic.py ${cfg}_rollout_n${envs}_chunk${chunk} $kern $d/pmc_fetch.csv $d/pmc_write.csv $d/pmc_rdreq.csv $d/pmc_sq1.csv $d/pmc_sq2.csv
 done
 cp profiles/pmc_traffic.json gpurun_out/pmc_traffic.json
