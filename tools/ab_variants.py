@@ -75,6 +75,11 @@ VARIANTS = {
             if (aout) __builtin_nontemporal_store(u32x4{aa[0], aa[1], aa[2], aa[3]}, reinterpret_cast<u32x4*>(aout + f));""",
                """            if (vout) *reinterpret_cast<u32x4*>(vout + f) = u32x4{vv[0], vv[1], vv[2], vv[3]};
             if (aout) *reinterpret_cast<u32x4*>(aout + f) = u32x4{aa[0], aa[1], aa[2], aa[3]};""")],
+    # the plane writer's piece loop unrolled twice (more stores in flight per wave)
+    "obsun2": [("sparc_kernels.hip", """    const uint32_t dl = 256u / XY, dc = 256u - dl * XY;   // a 64-piece stride in envs / cells
+    for (; f < total; f += 256u) {""", """    const uint32_t dl = 256u / XY, dc = 256u - dl * XY;   // a 64-piece stride in envs / cells
+#pragma unroll 2
+    for (; f < total; f += 256u) {""")],
     # k_rollout1r with s_memtime stamps (timing only: the stats buffer receives, per wave, role |
     # total | barrier-wait | audit cycles at index N/2 + block * 16 + wave; tools/diag_r1r.py)
     "stamps": [
