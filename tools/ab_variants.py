@@ -80,6 +80,9 @@ VARIANTS = {
     for (; f < total; f += 256u) {""", """    const uint32_t dl = 256u / XY, dc = 256u - dl * XY;   // a 64-piece stride in envs / cells
 #pragma unroll 2
     for (; f < total; f += 256u) {""")],
+    # k_rollout1s without the trie wave's priority (re-checked after IOR balanced the chains)
+    "noprio": [("sparc_kernels.hip", """        __builtin_amdgcn_s_setprio(1);
+        TrieLane tl;""", """        TrieLane tl;""")],
     # k_rollout1r with s_memtime stamps (timing only: the stats buffer receives, per wave, role |
     # total | barrier-wait | audit cycles at index N/2 + block * 16 + wave; tools/diag_r1r.py)
     "stamps": [
