@@ -3,7 +3,8 @@
 
 Workload (default, BASELINE.json configs[2]): 65,536 concurrent 7x7 SPaRC instances per GPU,
 full property set, traceback=True, max_steps=2000, gymnasium next-step autoreset onto the next
-puzzle, 1,024 synthetic puzzles (seed 0), env i -> puzzle (i * 2654435761) mod 1024.
+puzzle, 1,024 synthetic puzzles (seed 0; ``--puzzles P`` extends the pool by blocks of 1,024, block b
+drawn with seed b), env i -> puzzle (i * 2654435761) mod P.
 Actions are uniform random in {0,1,2,3}, generated on the GPU before the timed region (uint8
 tiles resident in HBM, like a policy's output) by the counter-based generator keyed by the
 global env id (sparc_random_actions_device), so N ranks hold the tiles of one process over all
@@ -112,6 +113,41 @@ def rule_rollout_kernel(proc, table):
             return "k_rollout"
         entries += 8 * (1 if cells <= 3 else 1 << (cells - 3))
     return "k_rollout1r" if entries <= 1 << 28 else "k_rollout"
+
+
+def _pool_block(args):
+    b, cnt, sizes, full = args
+    from sparc_gym_amd import synthetic
+    from sparc_gym_amd.puzzles import process_puzzles
+    return process_puzzles(synthetic.make_puzzles(cnt, seed=b, sizes=sizes, full_properties=full))
+
+
+def make_pool(P, sizes, full, workers=8):
+    """The bench's synthetic pool of P processed puzzles: blocks of 1,024 records, block b drawn
+    by synthetic.make_puzzles(seed=b), so the default 1,024-puzzle pool is block 0 and a larger
+    pool extends it.  Blocks are generated in worker processes (fork, before any GPU call;
+    SPARC_POOL_WORKERS=1: in this process, e.g. under a profiler that initialises the GPU
+    first).  SPARC_POOL_CACHE=<dir>: the pool is kept there as a pickle this function wrote."""
+    import pickle
+    cache = os.environ.get("SPARC_POOL_CACHE")
+    path = os.path.join(cache, f"pool_{P}_{'_'.join('%dx%d' % s for s in sizes)}_{int(bool(full))}.pkl") if cache else None
+    if path and os.path.exists(path):
+        with open(path, "rb") as f:
+            return pickle.load(f)
+    workers = int(os.environ.get("SPARC_POOL_WORKERS", workers))
+    blocks = [(b, min(1024, P - 1024 * b), sizes, full) for b in range((P + 1023) // 1024)]
+    if len(blocks) == 1 or workers <= 1:
+        pool = [p for blk in map(_pool_block, blocks) for p in blk]
+    else:
+        import concurrent.futures as cf
+        import multiprocessing as mp
+        with cf.ProcessPoolExecutor(min(workers, len(blocks)), mp_context=mp.get_context("fork")) as ex:
+            pool = [p for blk in ex.map(_pool_block, blocks) for p in blk]
+    if path:
+        os.makedirs(cache, exist_ok=True)
+        with open(path, "wb") as f:
+            pickle.dump(pool, f)
+    return pool
 
 
 def state_bytes_per_env(words, traceback):
@@ -395,11 +431,13 @@ def main():
     if world_env != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world_env}: the job would not measure "
                          f"{args.gpus} GPUs")
+    sizes, full, tb, obs = CONFIGS[args.config]
+    proc = make_pool(args.puzzles, sizes, full)   # before torch / any GPU call (worker processes fork)
     import torch
     import torch.distributed as dist
-    from sparc_gym_amd import SPaRCVecEnv, synthetic
+    from sparc_gym_amd import SPaRCVecEnv
     from sparc_gym_amd import dist as sdist
-    from sparc_gym_amd.puzzles import pack_table, process_puzzles
+    from sparc_gym_amd.puzzles import pack_table
 
     ndev = torch.cuda.device_count()
     local_env = int(os.environ.get("LOCAL_RANK", "0"))
@@ -418,11 +456,8 @@ def main():
         raise SystemExit(f"rank {rank}: world {world} (asked {args.gpus}), GPUs per rank {pci}: need one "
                          f"distinct GPU per rank (--rehearsal lets ranks share GPUs, for tests only)")
 
-    sizes, full, tb, obs = CONFIGS[args.config]
     if args.envs <= 0:
         args.envs = DEFAULT_ENVS[args.config]
-    recs = synthetic.make_puzzles(args.puzzles, seed=0, sizes=sizes, full_properties=full)
-    proc = process_puzzles(recs)
     table = pack_table(proc)
     offset, n = sdist.env_shard(args.envs, rank)
     vec = SPaRCVecEnv(n, processed=proc, table=table, traceback=tb, max_steps=args.max_steps,

@@ -80,6 +80,16 @@ VARIANTS = {
     for (; f < total; f += 256u) {""", """    const uint32_t dl = 256u / XY, dc = 256u - dl * XY;   // a 64-piece stride in envs / cells
 #pragma unroll 2
     for (; f < total; f += 256u) {""")],
+    # k_rollout1s with the move rows (mrow) read from global memory although the table fits LDS
+    "mrowg": [("sparc_kernels.hip", """        mrow = lm;
+        trow = lt;
+    }""", """        trow = lt;
+    }""")],
+    # k_rollout1s with the trie rows (trow) read from global memory although the table fits LDS
+    "trowg": [("sparc_kernels.hip", """        mrow = lm;
+        trow = lt;
+    }""", """        mrow = lm;
+    }""")],
     # k_rollout1s without the trie wave's priority (re-checked after IOR balanced the chains)
     "noprio": [("sparc_kernels.hip", """        __builtin_amdgcn_s_setprio(1);
         TrieLane tl;""", """        TrieLane tl;""")],

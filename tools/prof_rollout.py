@@ -10,16 +10,8 @@ sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "sparc-gym_amd"))
 
 import numpy as np  # noqa: E402
-import torch  # noqa: E402
 
-if "--lib" in sys.argv:   # another build of the library, loaded (after torch's HIP runtime) before the package uses it
-    torch.cuda.init()
-    from sparc_gym_amd import _lib as _sparc_lib  # noqa: E402
-    _sparc_lib.load(os.path.abspath(sys.argv[sys.argv.index("--lib") + 1]))
-
-import bench  # noqa: E402
-from sparc_gym_amd import SPaRCVecEnv, synthetic  # noqa: E402
-from sparc_gym_amd.puzzles import pack_table, process_puzzles  # noqa: E402
+import bench  # noqa: E402  (no torch import at module level)
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="c3")
@@ -31,10 +23,22 @@ ap.add_argument("--no-out", action="store_true", help="do not write reward codes
 ap.add_argument("--time", action="store_true", help="print the mean launch time (HIP events)")
 ap.add_argument("--lib", default=None, help="path of a diagnostic build of libsparc_gym_amd.so")
 ap.add_argument("--rules", action="store_true", help="the rule audit after every step (rollout(rules=True))")
+ap.add_argument("--puzzles", type=int, default=1024, help="pool size (bench.make_pool: blocks of 1,024)")
 a = ap.parse_args()
 sizes, full, tb, obs = bench.CONFIGS[a.config]
+proc = bench.make_pool(a.puzzles, sizes, full)   # before torch / any GPU call (worker processes fork)
+
+import torch  # noqa: E402
+
+if a.lib:   # another build of the library, loaded (after torch's HIP runtime) before the package uses it
+    torch.cuda.init()
+    from sparc_gym_amd import _lib as _sparc_lib  # noqa: E402
+    _sparc_lib.load(os.path.abspath(a.lib))
+
+from sparc_gym_amd import SPaRCVecEnv  # noqa: E402
+from sparc_gym_amd.puzzles import pack_table  # noqa: E402
+
 a.rules = a.rules or a.config in bench.RULE_CONFIGS
-proc = process_puzzles(synthetic.make_puzzles(1024, seed=0, sizes=sizes, full_properties=full))
 table = pack_table(proc)
 vec = SPaRCVecEnv(a.envs, processed=proc, table=table, traceback=tb, observation="compact", rules=a.rules)
 gid = np.arange(a.envs, dtype=np.uint64)
