@@ -104,7 +104,7 @@ def rule_rollout_kernel(proc, table):
     when the boards are one word, fit its ring word (x_size * pitch <= 57) and every puzzle has a
     region-code table (at most 12 cells, 2^(cells) entries each within the 2^28-entry budget);
     else the generic k_rollout<..., RULES>."""
-    if table.words != 1 or os.environ.get("SPARC_RULE_ROLLOUT") == "generic":
+    if table.words != 1:
         return "k_rollout"
     entries = 0
     for p in proc:

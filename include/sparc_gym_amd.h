@@ -197,8 +197,10 @@ int sparc_rollout_obs_device(void *ctx, int32_t T, const uint8_t *d_actions, uin
  * step() does (_validate_rules at SPaRC_Gym.py:1227 and again in _get_info 1011, filling
  * info['rule_status'], 941-950): d_rule_bits [T][N] uint16, step t's entry equal to
  * sparc_rules_device's bits after the t-th of T single steps.  Needs sparc_load_rules.  The
- * audit (flood fills, exact-fit searches) costs far more than the step; this path runs the
- * generic per-wave kernel. */
+ * audit (flood fills, exact-fit searches) costs far more than the step.  On one-word (5x5 /
+ * 7x7) pools whose every puzzle has a region-code table this runs k_rollout1r (per 64 envs a
+ * step wave and five audit waves); otherwise the generic per-wave rule kernel.  The bits are
+ * identical. */
 int sparc_rollout_rules_device(void *ctx, int32_t T, const uint8_t *d_actions, uint64_t seed, uint64_t t0,
                                int8_t *d_reward, uint8_t *d_flags, int32_t *d_stats, uint16_t *d_rule_bits);
 
@@ -290,6 +292,20 @@ int sparc_rules_finish(void *ctx, uint16_t *d_bits, uint64_t *d_fit);
  * (0: 2^28 = 128 MB; puzzles past it are audited by the memoised search instead).  The cap applies
  * to the following audits and the next sparc_load_rules, the budget to the next sparc_load_rules. */
 int sparc_set_rule_limits(void *ctx, uint32_t fit_cap_nodes, uint64_t table_entries);
+
+/* ---- debug: kernel variants (A/B runs and tests) ----------------------------------------------
+ * Selects, for this context, among kernel variants that compute identical results.  Callers never
+ * need it, and nothing else (no environment variable) changes the kernel a context runs.
+ *  SPARC_VARIANT_IO_CODES_OFF          1: under next-step autoreset the split rollouts keep the
+ *                                      reward codes on the trie wave (k_rollout1s / k_rolloutWs
+ *                                      without the I/O-wave codes); 0: default
+ *  SPARC_VARIANT_RULE_ROLLOUT_GENERIC  1: rule rollouts on the generic per-wave rule kernel even
+ *                                      where k_rollout1r applies; 0: default
+ *  SPARC_VARIANT_R1R_SHAPE             k_rollout1r's <G, A, RT>: 0 <2, 5, 10> (default),
+ *                                      1 <4, 3, 12>, 2 <2, 4, 12>
+ * SPARC_E_INVALID for another `which` or value. */
+enum { SPARC_VARIANT_IO_CODES_OFF = 1, SPARC_VARIANT_RULE_ROLLOUT_GENERIC = 2, SPARC_VARIANT_R1R_SHAPE = 3 };
+int sparc_set_variant(void *ctx, int32_t which, int32_t value);
 
 /* ---- multi-GPU: the end-of-batch gather over RCCL (xGMI) -------------------------------------
  * The envs shard across GPUs as contiguous global id ranges (env_offset), one process and one

@@ -127,6 +127,14 @@ __device__ __forceinline__ void bb_clear(uint64_t (&v)[W], uint32_t b) {
     for (int k = 0; k < W; ++k) v[k] &= ((b >> 6) == (uint32_t)k) ? ~m : ~0ull;
 }
 
+// element of a global table at a 32-bit byte offset: the load takes the table base in SGPRs and
+// the offset in one VGPR (global_load v, vOff, s[base:base+1]) instead of a 64-bit VGPR address
+// (tables are < 4 GiB: sparc_load_puzzles)
+template <class T>
+__device__ __forceinline__ T ld_off(const T* __restrict__ base, uint32_t byte_off) {
+    return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + byte_off);
+}
+
 __device__ __forceinline__ uint32_t uint_rand_action(uint64_t seed, uint64_t env, uint64_t t) {
     uint64_t z = seed + env * 0x9E3779B97F4A7C15ull + t * 0xD1B54A32D192ED03ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;

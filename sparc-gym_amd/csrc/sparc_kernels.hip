@@ -734,6 +734,9 @@ constexpr size_t kS_Base = kS_Fin + 4 * 64 * 2 * sizeof(uint4);
 static_assert(kS_Cnt + 3 * 256 * sizeof(int32_t) <= kS_Base, "k_rollout1s IOR counters");
 // LDS bytes of the staged rows: move rows + trie rows, 16 B each per puzzle
 __host__ __device__ constexpr size_t split_table_bytes(uint32_t P) { return (size_t)P * 2 * sizeof(uint4); }
+// LDS_TABLE = false (pools past the row budget): the trie rows' slots at kS_Base (sparc_move1.hpp)
+constexpr size_t kS_SlotBytes = (kRowSlots + 1) * kRowSlotStride;
+static_assert(kRowSlotStride == 256 * sizeof(uint4) && (kRowSlots & (kRowSlots - 1)) == 0, "row slots");
 
 // four action bytes with every byte >= 4 mapped to 4 (never legal: legal bit 4 is 0), so the
 // move wave tests legality with one shift
@@ -923,13 +926,16 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
     const uint32_t i = wg_base + pr * 64u + lane;
     uint8_t* pb = smem + pr * kS_Pair;
     uint4* fin = reinterpret_cast<uint4*>(smem + kS_Fin) + (IOR ? 1u : 2u) * (pr * 64u + lane);
+    // LDS_TABLE = false: this env's trie-row slots (row_slots, sparc_move1.hpp)
+    const uint32_t slot_addr = MoveLane1<TB>::lds_addr(smem + kS_Base + (size_t)(pr * 64u + lane) * sizeof(uint4));
     if (wv < 4) {                                                // ---- move waves
         MoveLane1<TB> m;
         uint8_t* col = pb + kS_Stk + lane;
         const uint32_t col_addr = MoveLane1<TB>::lds_addr(col);
         m.load(p, i, col, col_addr);
         const uint32_t pid0 = p.st.pid[i];
-        m.prefetch_reset(mrow, pid0 + 1 == NP ? 0u : pid0 + 1);
+        if constexpr (LDS_TABLE) m.prefetch_reset(mrow, pid0 + 1 == NP ? 0u : pid0 + 1);
+        else m.prefetch_reset_g(mrow, trow, pid0 + 1 == NP ? 0u : pid0 + 1);
         const uint32_t pend0 = m.pending ? 1u : 0u;
         const uint64_t gid = p.env_offset + i;
         uint32_t* th = reinterpret_cast<uint32_t*>(pb + kS_FH) + lane;
@@ -955,10 +961,12 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const uint32_t row = (uint32_t)(k * kTile + g + j) & (kRing - 1);
-                    m.reset_next(p, mrow, col_addr);
+                    if constexpr (LDS_TABLE) m.reset_next(p, mrow, col_addr);
+                    else m.reset_next_g(p, mrow, trow, col_addr, slot_addr);
                     th[row * 64] = m.step_pos(p, pv[j]);
                 }
             }
+            if constexpr (!LDS_TABLE) m.tile_end();
             __syncthreads();                                     // B_{k+1}
         }
         __syncthreads();                                         // B_{K+1}
@@ -998,8 +1006,13 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         __syncthreads();                                         // B_1 (interval 0: no tile yet)
         if constexpr (LA)
             if (K > 0) tl.prime(pb[kS_Act + lane], p.tab.trieg);   // step 0's action (tile 0, buffer 0)
+        if constexpr (!LDS_TABLE) {
+            tl.slot_addr = slot_addr;
+            tl.lim = kRowSlots;
+        }
         for (int32_t k = 1; k <= K; ++k) {
             const uint8_t* ta = pb + kS_Act + ((k - 1) % 3) * (kTile * 64) + lane;   // tile k-1's actions
+            if constexpr (!LDS_TABLE) tl.slot_read(kRowSlots, kRowSlotStride);   // written in interval k-1 or before
             // LA: tile k's first action is the look-ahead of tile k-1's last step; buffer k % 3
             // holds tile k during this interval (loaded by the I/O wave in the last one; after
             // the last tile it is stale, and that look-ahead is never used)
@@ -1020,10 +1033,12 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
                 for (int j = 0; j < 4; ++j) {
                     int code;
                     if constexpr (LA) code = tl.step1la<!IOR>(hb[j], av[j], av[j + 1], trow, p.tab.trieg, NP);
-                    else code = tl.step1<!IOR>(hb[j], av[j], trow, p.tab.trie8, NP);
+                    else if constexpr (LDS_TABLE) code = tl.step1<!IOR>(hb[j], av[j], trow, p.tab.trie8, NP);
+                    else code = tl.step1s<!IOR, kRowSlots, kRowSlotStride>(hb[j], av[j], trow, p.tab.trie8, NP);
                     tr[(row0 + j) * 64] = (uint8_t)code;
                 }
             }
+            if constexpr (!LDS_TABLE) tl.slot_tile_end(kRowSlots);
             __syncthreads();                                     // B_{k+1}
         }
         if constexpr (IOR)   // the last step's hand-over word is still in the ring
@@ -1577,9 +1592,10 @@ struct Ctx {
     uint64_t* r_rows = nullptr;   // the audit's per-puzzle rows (RulesTab::rows)
     bool r_tab_all = false;   // every puzzle has a region-code table (k_rollout1r's audit)
     bool ring_ok = false;     // W = 1 and every board fits below kRingShift (k_rollout1r's ring word)
-    bool rules_generic = false;   // SPARC_RULE_ROLLOUT=generic: rule rollouts on k_rollout<..., RULES> (A/B, tests)
-    bool io_codes_off = false;    // SPARC_IO_CODES=off: k_rollout1s keeps the reward codes on the trie wave (A/B, tests)
-    int r1r_shape = 0;            // SPARC_R1R_SHAPE: k_rollout1r's <G, A, RT> (0: <2, 5, 10>; 1, 2: A/B, tests)
+    // kernel variants with identical results, set only by sparc_set_variant (A/B runs, tests)
+    bool rules_generic = false;   // rule rollouts on k_rollout<..., RULES>
+    bool io_codes_off = false;    // k_rollout1s / k_rolloutWs keep the reward codes on the trie wave
+    int r1r_shape = 0;            // k_rollout1r's <G, A, RT> (0: <2, 5, 10>; 1, 2: A/B, tests)
     // exact-fit searches past the GPU's node cap (sparc_set_fit_cap) are finished on the host
     // from these copies of the rule table (sparc_rules.hpp exact_fit, the same code)
     uint32_t fit_cap = kFitCap;
@@ -1776,9 +1792,6 @@ int sparc_create(int device, const sparc_config* cfg, void** ctx_out) {
     c->device = device;
     c->n = (uint32_t)cfg->num_envs;
     c->W = cfg->words;
-    if (const char* v = getenv("SPARC_RULE_ROLLOUT")) c->rules_generic = strcmp(v, "generic") == 0;
-    if (const char* v = getenv("SPARC_R1R_SHAPE")) c->r1r_shape = atoi(v);
-    if (const char* v = getenv("SPARC_IO_CODES")) c->io_codes_off = strcmp(v, "off") == 0;
     const size_t n = c->n;
     auto cleanup = [&](int code) {
         sparc_destroy(c);
@@ -2223,7 +2236,8 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
             const int32_t T16 = T / kTile * kTile;
             const size_t sbytes = split_table_bytes(c->num_puzzles);
             const bool lds_s = kS_Base + sbytes <= budget;
-            const size_t shm_s = kS_Base + (lds_s ? sbytes : 0);
+            // past the row budget: rows from the L2, the trie rows handed over through slots
+            const size_t shm_s = kS_Base + (lds_s ? sbytes : kS_SlotBytes);
             auto launch_s = [&](auto kern, const uint8_t* a) {
                 if (shm_s > 64 * 1024 && (lds_rc = allow_big_lds(c, reinterpret_cast<const void*>(kern)))) return;
                 kern<<<dim3((unsigned)blocks), kBlock1s, shm_s, c->stream>>>(p, T16, a, seed, t0, d_rew, d_flags, st);
@@ -2705,6 +2719,28 @@ int sparc_rules_device(void* ctx, uint16_t* d_bits, uint8_t* d_region, uint64_t*
     else if (c->W == 2) k_rules<2><<<g, kBlock, 0, c->stream>>>(p, rt, d_bits, d_region, d_fit, c->r_memo);
     else k_rules<4><<<g, kBlock, 0, c->stream>>>(p, rt, d_bits, d_region, d_fit, c->r_memo);
     return launch_check(c);
+}
+
+int sparc_set_variant(void* ctx, int32_t which, int32_t value) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c) return fail(nullptr, SPARC_E_INVALID, "null context");
+    switch (which) {
+        case SPARC_VARIANT_IO_CODES_OFF:
+            if (value != 0 && value != 1) break;
+            c->io_codes_off = value == 1;
+            return SPARC_OK;
+        case SPARC_VARIANT_RULE_ROLLOUT_GENERIC:
+            if (value != 0 && value != 1) break;
+            c->rules_generic = value == 1;
+            return SPARC_OK;
+        case SPARC_VARIANT_R1R_SHAPE:
+            if (value < 0 || value > 2) break;
+            c->r1r_shape = value;
+            return SPARC_OK;
+        default:
+            return fail(c, SPARC_E_INVALID, "unknown variant");
+    }
+    return fail(c, SPARC_E_INVALID, "bad variant value");
 }
 
 int sparc_set_rule_limits(void* ctx, uint32_t fit_cap_nodes, uint64_t table_entries) {

@@ -38,6 +38,20 @@ namespace sparc {
 
 constexpr uint32_t kHwTerm = 0x10000u, kHwTrunc = 0x20000u, kHwReset = 0x400000u, kHwLegal = 0x3C0000u;
 
+// Row slots (k_rollout1s on pools past the LDS row budget).  The trie wave runs one tile behind
+// the move wave, so the move wave, which reads both rows of the next puzzle from the L2 at the
+// previous reset anyway, hands the trie row over through LDS: per env kRowSlots slots and one
+// spare, [kRowSlots + 1][256 envs] uint4.  The move wave writes reset r's row to slot r %
+// kRowSlots during the interval of its tile t_r; the trie wave reads it during interval t_r + 1
+// (reset ordinals r = 0, 1, ... count this launch's resets of the env; both waves count the same
+// events).  The write is allowed when the slot's previous occupant, reset r - kRowSlots, was read
+// in an earlier interval: t_(r - kRowSlots) <= t_r - 2, i.e. r < C(t_r - 2) + kRowSlots with C(t)
+// the resets in tiles <= t.  Both waves evaluate that rule from their own counts; when it fails
+// the move wave writes the spare slot instead and the trie wave reads the row from the L2 itself
+// (an episode of a few steps: two resets within two tiles).  Barriers separate every write from
+// its read and from the next write of the slot.
+constexpr uint32_t kRowSlots = 2, kRowSlotStride = 256u * 16u;
+
 // the carry-free gather constant and the neighbour mask of the window for pitch P (host and
 // device): window bits {2P, P-1, 0, P+1} -> product bits 18, 19, 20, 21 (right, up, left, down)
 __host__ __device__ constexpr uint32_t legal_magic(uint32_t P) {
@@ -66,6 +80,16 @@ struct MoveLane1 {
     uint32_t rp = 0, pnr = 0;             // traceback: back position of the last move / the one before
     uint32_t lv = 0x30000u;               // flag-bit mask of the step: term | trunc, or kHwReset
     uint4 rr = {0u, 0u, 0u, 0u};          // the next autoreset's move row: row word, free board, the puzzle after it
+    // global rows (k_rollout1s<…, LDS_TABLE = false>, row_slots below): the next autoreset's trie
+    // row, handed to the trie wave through its slot; this launch's reset count and the tile
+    // bookkeeping of the slot rule
+    // (4-vectors, so that each row keeps one register tuple through the loop and the next read
+    // lands in it: as a struct the compiler split the move row and copied the read's result into
+    // the pieces, waiting for the L2 in the reset branch)
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) v4u lds_v4;
+    v4u rg = {0u, 0u, 0u, 0u}, rt = {0u, 0u, 0u, 0u};
+    uint32_t nres = 0, lim = kRowSlots, cA = 0;
 
     typedef __attribute__((address_space(3))) uint8_t lds_u8;
     __device__ __forceinline__ static lds_u8* lds_byte(uint32_t a) { return (lds_u8*)(uintptr_t)a; }
@@ -107,6 +131,47 @@ struct MoveLane1 {
             __asm__ volatile("" ::"v"(fr), "v"(e), "v"(tgt), "v"(pflags) : "memory");
             rr = mrow[rr.w];
         }
+    }
+
+    // the same from global rows: the move row and the trie row of the next puzzle are read from
+    // the L2-resident tables into registers at the previous reset (the wave waits for them only
+    // at its next reset); the trie row goes on to the trie wave through slot nres % kRowSlots
+    // (row_slots), or to this lane's spare slot when the rule forbids the write
+    __device__ __forceinline__ void prefetch_reset_g(const uint4* __restrict__ mrow, const uint4* __restrict__ trow,
+                                                     uint32_t q) {
+        rg = ld_off(reinterpret_cast<const v4u*>(mrow), q << 4);
+        rt = ld_off(reinterpret_cast<const v4u*>(trow), q << 4);
+    }
+    __device__ __forceinline__ void reset_next_g(const Params& p, const uint4* __restrict__ mrow,
+                                                 const uint4* __restrict__ trow, uint32_t col_addr, uint32_t slot_addr) {
+        if ((pending != 0u) & (p.autoreset == 1)) {
+            e = rg.x & 0xFFu;
+            tgt = (rg.x >> 8) & 0xFFu;
+            pflags = rg.x >> 16;
+            fr = ((uint64_t)rg.z << 32) | rg.y;
+            w = 0;
+            if constexpr (TB) {
+                sp = col_addr;
+                set_bks(col_addr);
+                bias = 0;
+            } else {
+                len = 1;
+            }
+            step = -1;
+            lv = kHwReset;
+            const uint32_t s = nres < lim ? (nres & (kRowSlots - 1u)) : kRowSlots;
+            *(lds_v4*)(uintptr_t)(slot_addr + s * kRowSlotStride) = rt;
+            nres += 1u;
+            __asm__ volatile("" ::"v"(fr), "v"(e), "v"(tgt), "v"(pflags) : "memory");
+            const uint32_t q = rg.w << 4;
+            rg = ld_off(reinterpret_cast<const v4u*>(mrow), q);
+            rt = ld_off(reinterpret_cast<const v4u*>(trow), q);
+        }
+    }
+    // after each tile: lim = resets through the tile before last + kRowSlots (row_slots)
+    __device__ __forceinline__ void tile_end() {
+        lim = cA + kRowSlots;
+        cA = nres;
     }
 
     // one env-step's move part (1131-1199) from the target's window position; returns the

@@ -28,6 +28,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "sparc_env.hpp"
+
 namespace sparc {
 
 // per puzzle trie row: {root children right | up << 16, root children left | down << 16,
@@ -72,6 +74,54 @@ struct TrieLane {
         }
         npid = next_pid(q, num_puzzles);
         nx = trow[npid];
+    }
+
+    // ---- row slots (k_rollout1s on pools past the LDS row budget; sparc_move1.hpp row_slots):
+    // the next reset's trie row comes from the slot the move wave wrote, read at the start of
+    // each tile and after each reset (LDS reads, waited for with the step's other LDS reads), or
+    // from the L2 when the slot rule failed for that reset
+    uint32_t nres = 0, lim = 0, cA = 0, slot_addr = 0;
+    uint4 nxs = {0u, 0u, 0u, 0u};
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) v4u lds_v4;
+    __device__ __forceinline__ void slot_read(uint32_t slots, uint32_t stride) {
+        const v4u v = *(const lds_v4*)(uintptr_t)(slot_addr + (nres & (slots - 1u)) * stride);
+        nxs = make_uint4(v.x, v.y, v.z, v.w);
+    }
+    // after each tile (the same bookkeeping as MoveLane1::tile_end)
+    __device__ __forceinline__ void slot_tile_end(uint32_t slots) {
+        lim = cA + slots;
+        cA = nres;
+    }
+    template <bool CODES, uint32_t SLOTS, uint32_t STRIDE, class Rows>
+    __device__ __forceinline__ int step1s(const uint32_t hw, const uint32_t a, const Rows& trow,
+                                          const uint2* __restrict__ trie8, uint32_t num_puzzles) {
+        const bool reset = (hw & 0x400000u) != 0u;
+        const uint32_t dd = (uint32_t)((int32_t)hw >> 14) & 0xFFFF0000u;
+        const bool moved = hw >= 0x40000000u, done = (hw & 0x30000u) != 0u;
+        if (reset) {
+            const bool fb = nres >= lim;
+            pid = npid;
+            npid = next_pid(npid, num_puzzles);
+            apply_row(nxs);
+            nres += 1u;
+            if (fb) apply_row(ld_off(trow, pid << 4));   // the move wave wrote its spare slot: the L2 row
+        }
+        const int code = step_core<CODES>(false, dd, moved, done, a, trow, trie8, num_puzzles);
+        // the next reset's slot, in case that reset falls in this tile (at least two steps later:
+        // waited for with the LDS reads of a later step)
+        if (reset) slot_read(SLOTS, STRIDE);
+        return code;
+    }
+    __device__ __forceinline__ void apply_row(const uint4 r) {
+        rx = r.x;
+        ry = r.y;
+        base = r.z;
+        S = r.w & 0x18000u;
+        hs = (int32_t)((r.w >> 14) & 1u);
+        hsn = -hs;
+        hsb = (uint32_t)hs << 2;
+        tmax = r.w >> 17;
     }
 
     // ---- look-ahead form (k_rollout1s on small grids).  The trie wave runs a tile behind the
@@ -206,7 +256,7 @@ struct TrieLane {
         // trie on most steps).  Every field of a record holds a node of the same puzzle
         // (validated by sparc_load_puzzles), so no clamp here; load() clamps the stored node.
         if (take) {
-            const uint2 rec = trie8[base + (S & 0x7FFFu)];
+            const uint2 rec = ld_off(trie8, (base + (S & 0x7FFFu)) << 3);
             rx = rec.x;
             ry = rec.y;
         }

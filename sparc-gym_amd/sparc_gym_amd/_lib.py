@@ -74,6 +74,7 @@ _SIGS = {
     "sparc_rules_host": ([c_void_p, c_void_p, c_void_p, c_void_p], c_int32),
     "sparc_rules_finish": ([c_void_p, c_void_p, c_void_p], c_int32),
     "sparc_set_rule_limits": ([c_void_p, ctypes.c_uint32, c_uint64], c_int32),
+    "sparc_set_variant": ([c_void_p, c_int32, c_int32], c_int32),
     "sparc_comm_unique_id": ([c_void_p], c_int32),
     "sparc_comm_init": ([c_void_p, c_int32, c_int32, c_void_p, ctypes.POINTER(c_void_p)], c_int32),
     "sparc_comm_destroy": ([c_void_p], c_int32),

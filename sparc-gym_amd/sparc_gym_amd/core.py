@@ -88,6 +88,13 @@ class SparcCore:
         entries (0: 2^28); the budget applies at the next load_rules."""
         self._check(self.lib.sparc_set_rule_limits(self.ctx, int(fit_cap or 0), int(table_entries or 0)))
 
+    # sparc_set_variant (include/sparc_gym_amd.h): kernel variants with identical results
+    VARIANT_IO_CODES_OFF, VARIANT_RULE_ROLLOUT_GENERIC, VARIANT_R1R_SHAPE = 1, 2, 3
+
+    def set_variant(self, which, value):
+        """Debug: select a kernel variant of identical results for this context (A/B, tests)."""
+        self._check(self.lib.sparc_set_variant(self.ctx, int(which), int(value)))
+
     def close(self):
         if getattr(self, "ctx", None) is not None and self.ctx.value:
             self.lib.sparc_destroy(self.ctx)

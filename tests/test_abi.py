@@ -71,3 +71,24 @@ def test_missing_library_fails_loudly(tmp_path):
             _lib.load(str(tmp_path / "nope.so"))
         finally:
             _lib._lib = None
+
+
+def test_no_environment_variable_selects_a_kernel():
+    """Kernel variants (identical results; A/B runs and tests) are chosen only through the debug
+    entry point sparc_set_variant: the library reads no environment variable at all (it imports
+    neither getenv nor secure_getenv), so a stray variable cannot change the kernel a context
+    runs.  sparc_set_variant checks its arguments before touching the context."""
+    import shutil
+    import subprocess
+    nm = shutil.which("nm") or shutil.which("llvm-nm")
+    if nm is None:
+        pytest.skip("no nm")
+    undef = subprocess.run([nm, "-D", "--undefined-only", _lib.LIB_PATH], capture_output=True, text=True,
+                           check=True).stdout
+    imported = {line.split()[-1].split("@")[0] for line in undef.splitlines() if line.strip()}
+    assert not imported & {"getenv", "secure_getenv", "__secure_getenv"}, imported & {"getenv", "secure_getenv"}
+    lib = _lib.load()
+    assert lib.sparc_set_variant(None, 1, 1) == -1
+    src = open(os.path.join(REPO, "sparc-gym_amd", "csrc", "sparc_kernels.hip")).read()
+    for name in ("SPARC_IO_CODES", "SPARC_RULE_ROLLOUT", "SPARC_R1R_SHAPE"):
+        assert f'"{name}"' not in src

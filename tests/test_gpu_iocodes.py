@@ -9,9 +9,9 @@ to LDS at least every 128 tiles.  Checked bit-exact against the C oracle:
   outcome, i.e. Oneg after the launch, comes from TrieLane::finish_oneg), with and without
   traceback, so that both solved and failed done steps end launches;
 * one 4,160-step launch (260 tiles: two mid-launch counter flushes), stats and state;
-* the same launches with SPARC_IO_CODES=off (codes on the trie wave) give identical outputs.
+* the same launches with the codes on the trie wave (sparc_set_variant SPARC_VARIANT_IO_CODES_OFF)
+  give identical outputs.
 """
-import os
 
 import numpy as np
 import pytest
@@ -56,17 +56,9 @@ def _run(pool, tb, launches, T, io_off):
     from sparc_gym_amd import SPaRCVecEnv
     proc, table, opool = _pool(POOLS[pool])
     n = 1024
-    old = os.environ.get("SPARC_IO_CODES")
+    v = SPaRCVecEnv(n, processed=proc, table=table, traceback=tb, max_steps=2000, observation="compact")
     if io_off:
-        os.environ["SPARC_IO_CODES"] = "off"
-    try:
-        v = SPaRCVecEnv(n, processed=proc, table=table, traceback=tb, max_steps=2000, observation="compact")
-    finally:
-        if io_off:
-            if old is None:
-                os.environ.pop("SPARC_IO_CODES")
-            else:
-                os.environ["SPARC_IO_CODES"] = old
+        v.core.set_variant(v.core.VARIANT_IO_CODES_OFF, 1)
     v.reset(options={"puzzle_index": _pids(n)})
     st = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
     g = torch.Generator(device="cuda")

@@ -145,6 +145,8 @@ def test_rollout_rule_bits_every_step(on_gpu, sizes, max_shaped):
     pids = (np.arange(n) * 37) % len(proc)
     acts = torch.randint(0, 4, (T, n), dtype=torch.uint8, device="cuda")
     a = SPaRCVecEnv(n, **kw)
+    if generic:
+        a.core.set_variant(a.core.VARIANT_RULE_ROLLOUT_GENERIC, 1)
     a.reset(options={"puzzle_index": pids})
     ra = a.rollout(T, acts, rules=True)
     b = SPaRCVecEnv(n, **kw)
@@ -344,16 +346,14 @@ def test_exact_fit_fallback_queue_is_used_and_final(on_gpu):
 
 @pytest.mark.parametrize("budget", [None, 40 * 512])
 @pytest.mark.parametrize("generic", [False, True])
-def test_rules_table_budget_cutoff_mixed_pool(on_gpu, generic, budget, monkeypatch):
+def test_rules_table_budget_cutoff_mixed_pool(on_gpu, generic, budget):
     """budget 40 * 512: a region-code table budget that covers only the first 40 puzzles of a 7x7
     pool (sparc_load_rules stops at kMaxRegEntries), so the later puzzles are audited by the
     memoised search and one pool mixes table and search puzzles (the rule rollout then takes the
     generic kernel k_rollout<1, ..., RULES>).  budget None: every puzzle in the table (k_rollout1r,
-    or with SPARC_RULE_ROLLOUT=generic the generic kernel on the same pool).  With the node cap at 1
+    or with the SPARC_VARIANT_RULE_ROLLOUT_GENERIC variant the generic kernel on the same pool).  With the node cap at 1
     as well, every step of a rule rollout equals step()-by-step() audits, and samples equal the
     oracle."""
-    if generic:
-        monkeypatch.setenv("SPARC_RULE_ROLLOUT", "generic")
     from sparc_gym_amd import SPaRCVecEnv, synthetic
     from sparc_gym_amd.puzzles import process_puzzles
     recs = synthetic.make_rule_puzzles(96, seed=21, sizes=((3, 3),), break_prob=0.3)
@@ -365,6 +365,8 @@ def test_rules_table_budget_cutoff_mixed_pool(on_gpu, generic, budget, monkeypat
     pids = (np.arange(n) * 7) % len(proc)
     acts = torch.randint(0, 4, (T, n), dtype=torch.uint8, device="cuda")
     a = SPaRCVecEnv(n, **kw)
+    if generic:
+        a.core.set_variant(a.core.VARIANT_RULE_ROLLOUT_GENERIC, 1)
     a.reset(options={"puzzle_index": pids})
     ra = a.rollout(T, acts, rules=True)
     bits = ra["rule_bits"].cpu().numpy().astype(np.uint16)
@@ -384,8 +386,8 @@ def test_rules_table_budget_cutoff_mixed_pool(on_gpu, generic, budget, monkeypat
 
 
 @pytest.mark.parametrize("shape", [1, 2])
-def test_rule_rollout_shapes_equal_default(on_gpu, shape, monkeypatch):
-    """Every compiled shape of the W = 1 rule rollout (SPARC_R1R_SHAPE: k_rollout1r <G, A, RT> =
+def test_rule_rollout_shapes_equal_default(on_gpu, shape):
+    """Every compiled shape of the W = 1 rule rollout (sparc_set_variant SPARC_VARIANT_R1R_SHAPE: k_rollout1r <G, A, RT> =
     <4, 3, 12> and <2, 4, 12> besides the default <2, 5, 10>) gives the same
     reward codes, flags, stats, rule bits and final state as the default shape (oracle-pinned by
     test_rollout_rules_c3r_full_size), over two launches (the second with a partial last tile) on
@@ -401,8 +403,9 @@ def test_rule_rollout_shapes_equal_default(on_gpu, shape, monkeypatch):
     pids = (np.arange(n) * 13) % len(proc)
     acts = torch.randint(0, 5, (T1 + T2, n), dtype=torch.uint8, device="cuda")
 
-    def run():
+    def run(shape=0):
         v = SPaRCVecEnv(n, **kw)
+        v.core.set_variant(v.core.VARIANT_R1R_SHAPE, shape)
         v.reset(options={"puzzle_index": pids})
         st = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
         r1 = v.rollout(T1, acts[:T1], rules=True, stats=st)
@@ -411,8 +414,7 @@ def test_rule_rollout_shapes_equal_default(on_gpu, shape, monkeypatch):
         return [torch.cat([r1[k], r2[k]]).cpu().numpy() for k in ("reward_code", "flags", "rule_bits")], st.cpu().numpy(), s
 
     want, wst, ws = run()
-    monkeypatch.setenv("SPARC_R1R_SHAPE", str(shape))
-    got, gst, gs = run()
+    got, gst, gs = run(shape)
     for a, b in zip(got, want):
         assert np.array_equal(a, b)
     assert np.array_equal(gst, wst)
