@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define SPARC_ABI_VERSION 1
+#define SPARC_ABI_VERSION 2
 
 enum {
     SPARC_OK = 0,
@@ -231,13 +231,15 @@ int sparc_state_ptr(void *ctx, int32_t which, void **d_ptr);
  *              0-2 (count clamped to 7), star, square, coloured, colour 1..8, per-cell symbol
  *              multiplicity bits 0-2 (layers other than visited/gaps/agent/target set at a
  *              cell), y != 0, y != y_size-1, cells holding a poly/ylop instance
- *  inst_range  [P] first | count << 16 into inst (poly/ylop instances at cell centres,
- *              _extract_poly_instances 714-734)
- *  inst        bit | ylop << 10 | cx << 11 | cy << 14 | shape << 17
- *  shape_range [S] first offset | count << 16 into shape_off; shape_area [S] = sum of the
- *              shape array (722); shape_off [offsets][2] = (dx, dy) in cell units relative to
- *              the shape's anchor (_get_offsets 840-855)
- * Limits per puzzle: 16 ylops, 64 polys, 16 distinct poly shapes, lattice <= 15 x 15.         */
+ *  inst_first  [P + 1] offsets into inst: puzzle q's poly/ylop instances (at cell centres,
+ *              _extract_poly_instances 714-734) are inst[inst_first[q] .. inst_first[q + 1])
+ *  inst        bit | ylop << 10 | shape << 11 (shape < 2^21)
+ *  shape_first [S + 1] offsets into shape_off: shape s's cells are shape_off[shape_first[s] ..
+ *              shape_first[s + 1]), (dx, dy) in cell units relative to the shape's anchor
+ *              (_get_offsets 840-855); shape_area [S] = sum of the shape array (722)
+ * No pool-wide limit.  Lattices up to 15 x 15.  The exact-fit searches of a puzzle with more
+ * than 16 ylops or 16 distinct poly shapes (its instances' lists outgrow the GPU search's) run
+ * on the host (sparc_rules_finish), with the same search code; every answer is the same.      */
 #define SPARC_RULE_PLANES 25
 typedef struct {
     int32_t num_puzzles;    /* must equal the loaded step table's */
@@ -245,9 +247,9 @@ typedef struct {
     int32_t num_shapes;
     int32_t num_offsets;
     const uint64_t *planes;
-    const uint32_t *inst_range;
+    const uint32_t *inst_first;
     const uint32_t *inst;
-    const uint32_t *shape_range;
+    const uint32_t *shape_first;
     const int32_t *shape_area;
     const int8_t *shape_off;
 } sparc_rules_table;
@@ -279,13 +281,22 @@ int sparc_load_rules(void *ctx, const sparc_rules_table *table);
 int sparc_rules_device(void *ctx, uint16_t *d_bits, uint8_t *d_region, uint64_t *d_fit);
 int sparc_rules_host(void *ctx, uint16_t *bits, uint8_t *region, uint64_t *fit);
 
-/* Finish the exact-fit searches that passed the GPU's node cap in the LAST audit call
- * (sparc_rules_device, or sparc_rollout_rules_device: its d_rule_bits) on the host, without a
- * cap, and patch that call's outputs: SPARC_RULE_SEARCH_EXHAUSTED cleared, POLY_YLOP and ALL
- * cleared when a region does not fit, and (d_fit, may be NULL) the fit bits of the regions that
- * do.  Call it after each such call, before reading its bits (a no-op sync when nothing passed
- * the cap).  Synchronous.  SPARC_E_STATE when more than 65,536 searches of one call passed it. */
+/* Finish the exact-fit searches that passed the GPU's node cap (or belong to a puzzle whose
+ * searches run on the host) in the LAST audit call (sparc_rules_device, or
+ * sparc_rollout_rules_device: its d_rule_bits) on the host, without a cap, and patch that call's
+ * outputs on the device: SPARC_RULE_SEARCH_EXHAUSTED cleared, POLY_YLOP and ALL cleared when a
+ * region does not fit, and (d_fit, may be NULL) the fit bits of the regions that do.  Call it
+ * after each such call, before reading its bits, with that call's output pointers, and before its
+ * inputs change (a call that queued more searches than the queue holds is run again on a larger
+ * queue, from the state, stats and memo it started from).  Synchronous (a 4-byte read when
+ * nothing was queued).  SPARC_E_STATE: no audit call to finish, or bits of another call. */
 int sparc_rules_finish(void *ctx, uint16_t *d_bits, uint64_t *d_fit);
+
+/* out[3]: the exact-fit queue's capacity (65,536 entries at first, grown on overflow), the
+ * searches the last sparc_rules_finish ran on the host, and the audit calls run again so far
+ * because their searches overflowed the queue (diagnostics: how much of the audit went to the
+ * host). */
+int sparc_rules_queue_stats(void *ctx, uint64_t *out);
 
 /* Limits of the rule audit: fit_cap_nodes = search nodes one exact fit runs on the GPU before the
  * host finishes it (0: 2^26); table_entries = the region-code table budget in 4-bit entries

@@ -13,11 +13,13 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <type_traits>
 #include <vector>
 
@@ -513,11 +515,14 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
         if (!lead) {
             __hip_atomic_store(&pair_done[pair], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         } else {
-            // bounded: the partner runs the same loop and always gets here
-            for (uint32_t k = 0; k < (1u << 24) &&
-                                 __hip_atomic_load(&pair_done[pair], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u;
+            // bounded (the partner runs the same loop and always gets here; a bound keeps a fault
+            // from hanging the GPU): on timeout the context's error word reports it (sparc_sync)
+            uint32_t k = 0;
+            for (; k < (1u << 26) &&
+                   __hip_atomic_load(&pair_done[pair], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u;
                  ++k)
                 __builtin_amdgcn_s_sleep(2);
+            if (k == (1u << 26) && lane == 0) atomicOr(p.err, (int)kErrJoin);
         }
     }
     if (!active || !lead) return;
@@ -1550,7 +1555,39 @@ __global__ void __launch_bounds__(kBlock) k_region_table(Params p, RulesTab rt, 
     if (ex) atomicAdd(exhausted, ex);
 }
 
+// sparc_rules_finish's corrections of one output entry: rule bits &= ~clear, fit |= fit_or (the
+// host ran the queued exact-fit searches; every entry appears once)
+struct RulePatch {
+    uint64_t pos, fit_or;
+    uint32_t clear, pad;
+};
+__global__ void __launch_bounds__(kBlock) k_rule_patch(const RulePatch* __restrict__ pt, uint32_t count,
+                                                       uint16_t* __restrict__ bits, uint64_t* __restrict__ fit) {
+    const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
+    if (k >= count) return;
+    const RulePatch r = pt[k];
+    bits[r.pos] = (uint16_t)(bits[r.pos] & ~r.clear);
+    if (fit && r.fit_or) fit[r.pos] |= r.fit_or;
+}
+
 // ------------------------------------------------------------------------------ host side
+// The last audit call that may queue exact-fit searches (sparc_rules_finish): its outputs and
+// extent (entries: N, or T * N), and for a generic rule rollout its launch, so that a call whose
+// queue overflowed runs again on a larger queue from the state it started from (Ctx::snap).
+struct AuditCall {
+    int kind = 0;   // 0 none, 1 sparc_rules_device, 2 rule rollout (snapshot taken)
+    uint64_t extent = 0;
+    uint16_t* bits = nullptr;
+    uint8_t* region = nullptr;
+    uint64_t* fit = nullptr;
+    int32_t T = 0;
+    const uint8_t* act = nullptr;
+    uint64_t seed = 0, t0 = 0;
+    int8_t* rew = nullptr;
+    uint8_t* flags = nullptr;
+    int32_t* stats = nullptr;
+};
+
 struct Ctx {
     sparc_config cfg{};
     int device = 0;
@@ -1584,7 +1621,9 @@ struct Ctx {
     bool rules = false;
     uint64_t* r_planes = nullptr;   // [P][RP_COUNT][W] (sparc_rules.hpp: the ABI planes + derived ones)
     bool r_area = false;
-    uint32_t *r_inst_range = nullptr, *r_inst = nullptr, *r_shape_range = nullptr;
+    uint2* r_inst_fc = nullptr;     // [P] {first, count | kHostFit} (sparc_rules.hpp RulesTab)
+    uint32_t* r_inst = nullptr;
+    uint2* r_shape_range = nullptr;  // [S] {first offset, count}
     int32_t* r_shape_area = nullptr;
     int8_t* r_shape_off = nullptr;
     FitMemo<kMemo>* r_memo = nullptr;   // [N] per-env exact-fit memo of the audit (zeroed at sparc_load_rules)
@@ -1600,10 +1639,19 @@ struct Ctx {
     // from these copies of the rule table (sparc_rules.hpp exact_fit, the same code)
     uint32_t fit_cap = kFitCap;
     size_t reg_entries = (size_t)1 << 28;   // region-code table budget (entries of 4 bits)
-    std::vector<uint32_t> h_inst, h_inst_range, h_shape_range;
+    std::vector<uint32_t> h_inst;
+    std::vector<uint2> h_inst_fc, h_shape_range;
+    size_t host_fit_puzzles = 0;    // puzzles flagged kHostFit by the last sparc_load_rules
     std::vector<int8_t> h_shape_off;
     uint32_t* fq_count = nullptr;   // FitQueue of the audits (sparc_rules_finish)
     FitTodo* fq_items = nullptr;
+    uint32_t fq_cap = 0;            // its capacity (grown by sparc_rules_finish on overflow)
+    uint64_t fq_last = 0, fq_reruns = 0;   // searches the last finish ran; calls run again
+    uint32_t* h_count = nullptr;    // pinned host word the queue count is read into
+    AuditCall last_audit;           // the last queueing audit call (sparc_rules_finish)
+    // the state a generic rule rollout started from (re-run on a queue overflow)
+    void* snap = nullptr;
+    size_t snap_bytes = 0;
     uint16_t* s_bits = nullptr;
     uint8_t* s_region = nullptr;
     uint64_t* s_fit = nullptr;
@@ -1726,7 +1774,7 @@ constexpr uint32_t kFitQueueCap = 1u << 16;   // exact fits past the node cap pe
 RulesTab rules_tab(const Ctx* c, bool queue) {
     RulesTab rt{};
     rt.planes = c->r_planes;
-    rt.inst_range = c->r_inst_range;
+    rt.inst_fc = c->r_inst_fc;
     rt.inst = c->r_inst;
     rt.shape_range = c->r_shape_range;
     rt.shape_area = c->r_shape_area;
@@ -1736,7 +1784,7 @@ RulesTab rules_tab(const Ctx* c, bool queue) {
     rt.fit_cap = c->fit_cap;
     rt.reg_off = c->r_reg_off;
     rt.reg_tab = c->r_reg_tab;
-    rt.fq = FitQueue{queue ? c->fq_count : nullptr, c->fq_items, kFitQueueCap};
+    rt.fq = FitQueue{queue ? c->fq_count : nullptr, c->fq_items, c->fq_cap};
     rt.rows = c->r_rows;
     return rt;
 }
@@ -1751,15 +1799,32 @@ int host_fit_w(const Ctx* c, uint32_t q, uint64_t rm) {
     rt.inst = c->h_inst.data();
     rt.shape_range = c->h_shape_range.data();
     rt.shape_off = c->h_shape_off.data();
-    const FitIn fin = fit_in(rt, c->h_inst_range[q], X, Y);
+    const uint2 fc = c->h_inst_fc[q];
+    const FitIn fin = fit_in(rt, fc.x, fc.y & ~kHostFit, X, Y);
     const uint32_t P = (uint32_t)c->cfg.pitch;
     BB<W> Rc = BB<W>::zero();
     for (uint32_t b = 0; b < fin.CX * fin.CY; ++b)
         if ((rm >> b) & 1ull) Rc.set((2 * (b / fin.CY) + 1) * P + 2 * (b % fin.CY) + 1);
+    // a kHostFit puzzle: the same search with lists and counters sized for any puzzle
+    if (fc.y & kHostFit) return exact_fit<W, uint64_t, kHostFitMax, kHostFitMax, kHostFitPlanes>(fin, Rc, rm, ~0ull);
     return exact_fit<W, uint64_t>(fin, Rc, rm, ~0ull);
 }
 int host_fit(const Ctx* c, uint32_t q, uint64_t rm) {
     return c->W == 1 ? host_fit_w<1>(c, q, rm) : c->W == 2 ? host_fit_w<2>(c, q, rm) : host_fit_w<4>(c, q, rm);
+}
+
+// fn(k) for k in [0, n) on up to 16 host threads (the host's exact-fit searches)
+template <class F>
+void parallel_for(size_t n, F&& fn) {
+    std::atomic<size_t> next{0};
+    auto work = [&]() {
+        for (size_t k; (k = next.fetch_add(1)) < n;) fn(k);
+    };
+    const size_t nt = std::min<size_t>({n, 16, (size_t)std::max(1u, std::thread::hardware_concurrency())});
+    std::vector<std::thread> pool;
+    for (size_t k = 1; k < nt; ++k) pool.emplace_back(work);
+    work();
+    for (auto& th : pool) th.join();
 }
 
 }  // namespace
@@ -1825,10 +1890,12 @@ int sparc_destroy(void* ctx) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->vis, c->dirs, c->pos, c->aux, c->step, c->pid, c->t_open, c->t_info, c->t_root, c->t_trie, c->t_init, c->t_row1,
-                    c->t_trie8, c->t_trow, c->t_mrow, c->t_mroww, c->t_boardw, c->err, c->s_act, c->s_flags, c->s_mask, c->s_rew, c->s_pidx, c->r_planes, c->r_inst_range,
+                    c->t_trie8, c->t_trow, c->t_mrow, c->t_mroww, c->t_boardw, c->err, c->s_act, c->s_flags, c->s_mask, c->s_rew, c->s_pidx, c->r_planes, c->r_inst_fc,
                     c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off, c->r_memo, c->s_bits, c->s_region, c->s_fit, c->r_reg_off, c->r_reg_tab, c->fq_count, c->fq_items, c->r_rows};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
+    if (c->snap) (void)hipFree(c->snap);
+    if (c->h_count) (void)hipHostFree(c->h_count);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
     return SPARC_OK;
@@ -1862,6 +1929,7 @@ int sparc_sync(void* ctx) {
         HIPCHK(c, hipMemset(c->err, 0, sizeof(int32_t)));
         if (e & 2) return fail(c, SPARC_E_STATE, "device-side trie node out of range (state corrupted)");
         if (e & 8) return fail(c, SPARC_E_STATE, "rule audit: env puzzle index outside the rule table");
+        if (e & kErrJoin) return fail(c, SPARC_E_STATE, "rule rollout: an audit wave pair did not join (outputs unreliable)");
         return fail(c, SPARC_E_INVALID, "device-side puzzle index out of range in a reset");
     }
     return SPARC_OK;
@@ -2203,6 +2271,10 @@ int sparc_random_actions_device(void* ctx, int32_t T, uint64_t seed, uint64_t t0
 }  // extern "C"
 
 namespace {
+// rule rollouts that run k_rollout1r (W = 1 pools whose every puzzle has a region-code table and
+// whose boards fit the ring word); the rest run the generic k_rollout<..., RULES>
+bool r1r_rollout(const Ctx* c) { return c->W == 1 && c->r_tab_all && c->ring_ok && !c->rules_generic; }
+
 // sparc_rollout_device / sparc_rollout_obs_device; `ot` non-null: observation traces
 int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_t t0, int8_t* d_rew,
                  uint8_t* d_flags, int32_t* d_stats, const ObsTrace* ot, const RuleTrace* rtr = nullptr) {
@@ -2295,7 +2367,7 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
         if (lds_rc) return lds_rc;
         return launch_check(c);
     }
-    if (rtr && c->W == 1 && c->r_tab_all && c->ring_ok && !c->rules_generic) {
+    if (rtr && r1r_rollout(c)) {
         // rule rollouts of W = 1 pools with every puzzle in the region-code table: step waves +
         // audit waves (k_rollout1r; shape <G, A, RT> = c->r1r_shape)
         auto go_shape = [&](auto geo_c) {
@@ -2420,6 +2492,48 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
     return launch_check(c);
 }
 
+// The state, exact-fit memo and stats a generic rule rollout starts from, saved to / restored from
+// Ctx::snap on the context's stream (sparc_rules_finish re-runs a call whose queue overflowed)
+int snapshot(Ctx* c, int32_t* d_stats, bool save) {
+    const size_t n = c->n, W = (size_t)c->W;
+    const std::pair<void*, size_t> parts[] = {
+        {c->vis, 8 * W * n}, {c->dirs, c->cfg.traceback ? 16 * W * n : 0}, {c->pos, 4 * n}, {c->aux, 4 * n},
+        {c->step, 4 * n}, {c->pid, 4 * n}, {c->r_memo, sizeof(FitMemo<kMemo>) * n}, {d_stats, d_stats ? 16 * n : 0}};
+    size_t total = 0;
+    for (const auto& pt : parts) total += (pt.first ? pt.second : 0);
+    if (save && total > c->snap_bytes) {
+        if (c->snap) HIPCHK(c, hipFree(c->snap));
+        c->snap = nullptr;
+        c->snap_bytes = 0;
+        HIPCHK(c, hipMalloc(&c->snap, total));
+        c->snap_bytes = total;
+    }
+    size_t off = 0;
+    for (const auto& pt : parts) {
+        if (!pt.first || !pt.second) continue;
+        uint8_t* sp = static_cast<uint8_t*>(c->snap) + off;
+        if (save) HIPCHK(c, hipMemcpyAsync(sp, pt.first, pt.second, hipMemcpyDeviceToDevice, c->stream));
+        else HIPCHK(c, hipMemcpyAsync(pt.first, sp, pt.second, hipMemcpyDeviceToDevice, c->stream));
+        off += pt.second;
+    }
+    return SPARC_OK;
+}
+
+// launch the recorded audit call (sparc_rules_device / sparc_rollout_rules_device)
+int launch_rules(Ctx* c, const AuditCall& a) {
+    if (a.kind == 2) {
+        const RuleTrace rtr{rules_tab(c, true), a.bits, c->r_memo};
+        return rollout_impl(c, a.T, a.act, a.seed, a.t0, a.rew, a.flags, a.stats, nullptr, &rtr);
+    }
+    const Params p = make_params(c);
+    const RulesTab rt = rules_tab(c, true);
+    const dim3 g = grid_for(c->n);
+    if (c->W == 1) k_rules<1><<<g, kBlock, 0, c->stream>>>(p, rt, a.bits, a.region, a.fit, c->r_memo);
+    else if (c->W == 2) k_rules<2><<<g, kBlock, 0, c->stream>>>(p, rt, a.bits, a.region, a.fit, c->r_memo);
+    else k_rules<4><<<g, kBlock, 0, c->stream>>>(p, rt, a.bits, a.region, a.fit, c->r_memo);
+    return launch_check(c);
+}
+
 int check_obs_dims(Ctx* c, int32_t xd, int32_t yd) {
     if (xd < 1 || yd < 1 || (uint32_t)xd * (uint32_t)yd > kObsCells)
         return fail(c, SPARC_E_INVALID, "observation planes need x_dim, y_dim >= 1 and x_dim * y_dim <= 256");
@@ -2455,8 +2569,27 @@ int sparc_rollout_rules_device(void* ctx, int32_t T, const uint8_t* d_act, uint6
     if (rc) return rc;
     if (!c->rules) return fail(c, SPARC_E_STATE, "sparc_load_rules has not been called");
     if (!d_rule_bits) return fail(c, SPARC_E_INVALID, "null rule_bits");
-    const RuleTrace rtr{rules_tab(c, true), d_rule_bits, c->r_memo};
-    return rollout_impl(c, T, d_act, seed, t0, d_rew, d_flags, d_stats, nullptr, &rtr);
+    if (T < 0) return fail(c, SPARC_E_INVALID, "T must be >= 0");
+    HIPCHK(c, hipMemsetAsync(c->fq_count, 0, sizeof(uint32_t), c->stream));
+    AuditCall a;
+    a.kind = 2;
+    a.extent = (uint64_t)T * c->n;
+    a.bits = d_rule_bits;
+    a.T = T;
+    a.act = d_act;
+    a.seed = seed;
+    a.t0 = t0;
+    a.rew = d_rew;
+    a.flags = d_flags;
+    a.stats = d_stats;
+    c->last_audit = a;
+    // the generic rule kernel queues searches past the node cap: keep the state it starts from, so
+    // that sparc_rules_finish can run the call again on a larger queue (k_rollout1r never queues)
+    if (!r1r_rollout(c)) {
+        rc = snapshot(c, d_stats, true);
+        if (rc) return rc;
+    }
+    return launch_rules(c, a);
 }
 
 int sparc_step_obs_device(void* ctx, const uint8_t* d_act, int8_t* d_rew, uint8_t* d_flags, int32_t* d_visited,
@@ -2523,55 +2656,66 @@ int sparc_load_rules(void* ctx, const sparc_rules_table* t) {
     Ctx* c = static_cast<Ctx*>(ctx);
     int rc = check_ctx(c, false);
     if (rc) return rc;
-    if (!t || !t->planes || !t->inst_range) return fail(c, SPARC_E_INVALID, "null argument");
+    if (!t || !t->planes || !t->inst_first || !t->shape_first) return fail(c, SPARC_E_INVALID, "null argument");
     if ((uint32_t)t->num_puzzles != c->num_puzzles)
         return fail(c, SPARC_E_INVALID, "rule table puzzle count differs from the loaded puzzle table");
-    if (t->num_inst < 0 || t->num_shapes < 0 || t->num_offsets < 0 || t->num_offsets > 0xFFFF ||
-        t->num_shapes >= (1 << 15) || (t->num_inst && !t->inst) ||
-        (t->num_shapes && (!t->shape_range || !t->shape_area)) || (t->num_offsets && !t->shape_off))
+    if (t->num_inst < 0 || t->num_shapes < 0 || t->num_offsets < 0 || t->num_shapes >= (1 << 21) ||
+        (t->num_inst && !t->inst) || (t->num_shapes && !t->shape_area) || (t->num_offsets && !t->shape_off))
         return fail(c, SPARC_E_INVALID, "bad rule table sizes");
     const int W = c->W;
-    const size_t P = (size_t)t->num_puzzles;
+    const size_t P = (size_t)t->num_puzzles, S = (size_t)t->num_shapes;
     std::vector<uint4> info(P);
     HIPCHK(c, hipMemcpy(info.data(), c->t_info, sizeof(uint4) * P, hipMemcpyDeviceToHost));
-    for (int sh = 0; sh < t->num_shapes; ++sh) {
-        const uint32_t o0 = t->shape_range[sh] & 0xFFFFu, n = t->shape_range[sh] >> 16;
-        if (o0 + n > (uint32_t)t->num_offsets) return fail(c, SPARC_E_INVALID, "shape offsets out of range");
+    // the device's ranges: {first, count} per shape and {first, count | kHostFit} per puzzle
+    std::vector<uint2> srange(std::max<size_t>(1, S), make_uint2(0u, 0u)), ifc(P);
+    if (t->shape_first[0] != 0) return fail(c, SPARC_E_INVALID, "shape offsets must start at 0");
+    for (size_t sh = 0; sh < S; ++sh) {
+        const uint32_t o0 = t->shape_first[sh], o1 = t->shape_first[sh + 1];
+        if (o1 < o0 || o1 > (uint32_t)t->num_offsets) return fail(c, SPARC_E_INVALID, "shape offsets out of range");
+        srange[sh] = make_uint2(o0, o1 - o0);
     }
+    if (t->inst_first[0] != 0) return fail(c, SPARC_E_INVALID, "instance offsets must start at 0");
+    size_t host_fit_puzzles = 0;
     for (size_t q = 0; q < P; ++q) {
         const uint32_t X = info[q].x & 0xFFu, Y = (info[q].x >> 8) & 0xFFu;
-        const uint32_t f = t->inst_range[q] & 0xFFFFu, n = t->inst_range[q] >> 16;
+        const uint32_t f = t->inst_first[q], f1 = t->inst_first[q + 1];
         char m[160];
         if (X > 15 || Y > 15) {
             snprintf(m, sizeof m, "puzzle %zu: the rule audit supports lattices up to 15x15", q);
             return fail(c, SPARC_E_INVALID, m);
         }
-        if ((uint64_t)f + n > (uint64_t)t->num_inst) return fail(c, SPARC_E_INVALID, "instance range out of bounds");
-        int ny = 0, np = 0, nd = 0;
-        uint32_t ds[kFitShapes + 1];
-        for (uint32_t k = 0; k < n; ++k) {
-            const uint32_t e = t->inst[f + k], b = e & 0x3FFu, sh = e >> 17;
-            if (b >= 64u * W || sh >= (uint32_t)t->num_shapes) return fail(c, SPARC_E_INVALID, "bad instance");
-            if ((e >> 10) & 1u) { ++ny; continue; }
-            ++np;
-            int j = 0;
-            while (j < nd && ds[j] != sh) ++j;
-            if (j == nd && nd <= kFitShapes) ds[nd++] = sh;
-        }
-        if (ny > kFitYlops || np > kFitDepth || nd > kFitShapes) {
-            snprintf(m, sizeof m, "puzzle %zu: %d ylops / %d polys / %d poly shapes exceed 16 / 64 / 16", q, ny, np, nd);
+        if (f1 < f || f1 > (uint32_t)t->num_inst) return fail(c, SPARC_E_INVALID, "instance range out of bounds");
+        const uint32_t n = f1 - f;
+        const uint32_t cells = ((X - 1) / 2) * ((Y - 1) / 2);
+        if (n > cells) {   // _extract_poly_instances: one instance per cell centre
+            snprintf(m, sizeof m, "puzzle %zu: %u instances on %u cells", q, n, cells);
             return fail(c, SPARC_E_INVALID, m);
         }
+        int ny = 0, nd = 0;
+        uint32_t ds[kHostFitMax];
+        for (uint32_t k = 0; k < n; ++k) {
+            const uint32_t e = t->inst[f + k], b = e & 0x3FFu, sh = e >> 11;
+            if (b >= 64u * W || sh >= (uint32_t)S) return fail(c, SPARC_E_INVALID, "bad instance");
+            if ((e >> 10) & 1u) { ++ny; continue; }
+            int j = 0;
+            while (j < nd && ds[j] != sh) ++j;
+            if (j == nd) ds[nd++] = sh;
+        }
+        // past the GPU search's list sizes: the puzzle's searches run on the host (kHostFit)
+        const bool hf = ny > kFitYlops || nd > kFitShapes;
+        host_fit_puzzles += hf;
+        ifc[q] = make_uint2(f, n | (hf ? kHostFit : 0u));
     }
-    void* old[] = {c->r_planes, c->r_inst_range, c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off,
+    void* old[] = {c->r_planes, c->r_inst_fc, c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off,
                    c->r_reg_off, c->r_reg_tab, c->r_rows};
     for (void* b : old)
         if (b) HIPCHK(c, hipFree(b));
-    c->r_planes = nullptr; c->r_inst_range = nullptr; c->r_inst = nullptr;
+    c->r_planes = nullptr; c->r_inst_fc = nullptr; c->r_inst = nullptr;
     c->r_shape_range = nullptr; c->r_shape_area = nullptr; c->r_shape_off = nullptr;
     c->r_reg_off = nullptr; c->r_reg_tab = nullptr; c->r_rows = nullptr;
     c->rules = false;
     c->r_tab_all = false;
+    c->host_fit_puzzles = host_fit_puzzles;
     // the device copy: the caller's SPARC_RULE_PLANES planes per puzzle, RP_INST rewritten from the
     // instance list, then the bit-sliced net area of each cell (kAreaPlanes planes, sparc_rules.hpp)
     static_assert(RP_ABI == SPARC_RULE_PLANES, "rule plane layout");
@@ -2583,10 +2727,10 @@ int sparc_load_rules(void* ctx, const sparc_rules_table* t) {
         std::copy(t->planes + q * RP_ABI * W, t->planes + (q + 1) * RP_ABI * W, d);
         for (int k = 0; k < W; ++k) d[RP_INST * W + k] = 0;
         int32_t net[256] = {0};
-        const uint32_t f = t->inst_range[q] & 0xFFFFu, n = t->inst_range[q] >> 16;
+        const uint32_t f = ifc[q].x, n = ifc[q].y & ~kHostFit;
         for (uint32_t k = 0; k < n; ++k) {
             const uint32_t e = t->inst[f + k], b = e & 0x3FFu;
-            const int64_t a = t->shape_area[e >> 17];
+            const int64_t a = t->shape_area[e >> 11];
             net[b] = (int32_t)std::max<int64_t>(-(1 << 20), std::min<int64_t>(1 << 20, net[b] + (((e >> 10) & 1u) ? -a : a)));
             d[RP_INST * W + (b >> 6)] |= 1ull << (b & 63);
         }
@@ -2599,33 +2743,32 @@ int sparc_load_rules(void* ctx, const sparc_rules_table* t) {
     const size_t ni = std::max<size_t>(1, t->num_inst), ns = std::max<size_t>(1, t->num_shapes),
                  no = std::max<size_t>(1, t->num_offsets);
     HIPCHK(c, hipMalloc(&c->r_planes, sizeof(uint64_t) * np_));
-    HIPCHK(c, hipMalloc(&c->r_inst_range, sizeof(uint32_t) * P));
+    HIPCHK(c, hipMalloc(&c->r_inst_fc, sizeof(uint2) * P));
     HIPCHK(c, hipMalloc(&c->r_inst, sizeof(uint32_t) * ni));
-    HIPCHK(c, hipMalloc(&c->r_shape_range, sizeof(uint32_t) * ns));
+    HIPCHK(c, hipMalloc(&c->r_shape_range, sizeof(uint2) * ns));
     HIPCHK(c, hipMalloc(&c->r_shape_area, sizeof(int32_t) * ns));
     HIPCHK(c, hipMalloc(&c->r_shape_off, 2 * no));
     HIPCHK(c, hipMemcpy(c->r_planes, dev_planes.data(), sizeof(uint64_t) * np_, hipMemcpyHostToDevice));
     c->r_area = area_ok;   // a cell's net area outside -128..127: the audit walks the list instead
-    HIPCHK(c, hipMemcpy(c->r_inst_range, t->inst_range, sizeof(uint32_t) * P, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->r_inst_fc, ifc.data(), sizeof(uint2) * P, hipMemcpyHostToDevice));
     if (t->num_inst) HIPCHK(c, hipMemcpy(c->r_inst, t->inst, sizeof(uint32_t) * t->num_inst, hipMemcpyHostToDevice));
-    if (t->num_shapes) {
-        HIPCHK(c, hipMemcpy(c->r_shape_range, t->shape_range, sizeof(uint32_t) * t->num_shapes, hipMemcpyHostToDevice));
-        HIPCHK(c, hipMemcpy(c->r_shape_area, t->shape_area, sizeof(int32_t) * t->num_shapes, hipMemcpyHostToDevice));
-    }
+    HIPCHK(c, hipMemcpy(c->r_shape_range, srange.data(), sizeof(uint2) * ns, hipMemcpyHostToDevice));
+    if (S) HIPCHK(c, hipMemcpy(c->r_shape_area, t->shape_area, sizeof(int32_t) * S, hipMemcpyHostToDevice));
     if (t->num_offsets) HIPCHK(c, hipMemcpy(c->r_shape_off, t->shape_off, 2 * (size_t)t->num_offsets, hipMemcpyHostToDevice));
-    // host copies for the exact fits the host finishes (searches past the node cap)
+    // host copies for the exact fits the host finishes (searches past the node cap, kHostFit puzzles)
     c->h_inst.assign(t->inst, t->inst + t->num_inst);
     c->h_inst.resize(ni, 0u);
-    c->h_inst_range.assign(t->inst_range, t->inst_range + P);
-    c->h_shape_range.assign(t->shape_range, t->shape_range + t->num_shapes);
-    c->h_shape_range.resize(ns, 0u);
+    c->h_inst_fc = ifc;
+    c->h_shape_range = srange;
     c->h_shape_off.assign(t->shape_off, t->shape_off + 2 * (size_t)t->num_offsets);
     c->h_shape_off.resize(2 * no, 0);
     if (!c->fq_count) {
         HIPCHK(c, hipMalloc(&c->fq_count, sizeof(uint32_t)));
         HIPCHK(c, hipMalloc(&c->fq_items, sizeof(FitTodo) * kFitQueueCap));
+        c->fq_cap = kFitQueueCap;
     }
     HIPCHK(c, hipMemset(c->fq_count, 0, sizeof(uint32_t)));
+    c->last_audit = AuditCall{};
     // the memo's entries name puzzles of the old table: start empty (a zero key matches no region)
     if (!c->r_memo) HIPCHK(c, hipMalloc(&c->r_memo, sizeof(FitMemo<kMemo>) * (size_t)c->n));
     HIPCHK(c, hipMemset(c->r_memo, 0, sizeof(FitMemo<kMemo>) * (size_t)c->n));
@@ -2676,7 +2819,8 @@ int sparc_load_rules(void* ctx, const sparc_rules_table* t) {
             HIPCHK(c, hipMemset(c->fq_count, 0, sizeof(uint32_t)));
             std::vector<uint32_t> tab(words);
             HIPCHK(c, hipMemcpy(tab.data(), c->r_reg_tab, sizeof(uint32_t) * words, hipMemcpyDeviceToHost));
-            for (const uint2& it : items) {
+            parallel_for(items.size(), [&](size_t k) {   // each word belongs to one item
+                const uint2 it = items[k];
                 uint32_t& w = tab[reg_off[it.x] / 8u + it.y];
                 for (uint32_t j = 0; j < 8; ++j) {
                     const uint32_t sh = 4u * j + kRcPolyShift;
@@ -2684,7 +2828,7 @@ int sparc_load_rules(void* ctx, const sparc_rules_table* t) {
                     const uint32_t poly = host_fit(c, it.x, 8ull * it.y + j) ? 1u : 2u;
                     w = (w & ~(3u << sh)) | (poly << sh);
                 }
-            }
+            });
             HIPCHK(c, hipMemcpy(c->r_reg_tab, tab.data(), sizeof(uint32_t) * words, hipMemcpyHostToDevice));
         }
     }
@@ -2696,8 +2840,10 @@ int sparc_load_rules(void* ctx, const sparc_rules_table* t) {
             uint64_t* r = rows.data() + q * RW;
             for (int k = 0; k < 10; ++k)
                 for (int w = 0; w < W; ++w) r[k * W + w] = dev_planes[(q * RP_COUNT + kBasePlanes[k]) * W + w];
-            r[10 * W] = (uint64_t)reg_off[q] | ((uint64_t)t->inst_range[q] << 32);
-            r[10 * W + 1] = (uint64_t)info[q].x | ((uint64_t)info[q].y << 32);
+            // info.y bits 24-31 (free: flags use 16-18) carry the instance count | kHostFit << 7
+            const uint32_t cf = (ifc[q].y & 0x7Fu) | ((ifc[q].y & kHostFit) ? 0x80u : 0u);
+            r[10 * W] = (uint64_t)reg_off[q] | ((uint64_t)ifc[q].x << 32);
+            r[10 * W + 1] = (uint64_t)info[q].x | ((uint64_t)((info[q].y & 0x00FFFFFFu) | (cf << 24)) << 32);
         }
         HIPCHK(c, hipMalloc(&c->r_rows, sizeof(uint64_t) * rows.size()));
         HIPCHK(c, hipMemcpy(c->r_rows, rows.data(), sizeof(uint64_t) * rows.size(), hipMemcpyHostToDevice));
@@ -2712,13 +2858,26 @@ int sparc_rules_device(void* ctx, uint16_t* d_bits, uint8_t* d_region, uint64_t*
     int rc = check_ctx(c, true);
     if (rc) return rc;
     if (!c->rules) return fail(c, SPARC_E_STATE, "sparc_load_rules has not been called");
-    const Params p = make_params(c);
-    const RulesTab rt = rules_tab(c, true);
-    const dim3 g = grid_for(c->n);
-    if (c->W == 1) k_rules<1><<<g, kBlock, 0, c->stream>>>(p, rt, d_bits, d_region, d_fit, c->r_memo);
-    else if (c->W == 2) k_rules<2><<<g, kBlock, 0, c->stream>>>(p, rt, d_bits, d_region, d_fit, c->r_memo);
-    else k_rules<4><<<g, kBlock, 0, c->stream>>>(p, rt, d_bits, d_region, d_fit, c->r_memo);
-    return launch_check(c);
+    // a fresh queue for this call (a caller that skipped sparc_rules_finish leaves no entries that
+    // name another call's outputs), and the call recorded for sparc_rules_finish
+    HIPCHK(c, hipMemsetAsync(c->fq_count, 0, sizeof(uint32_t), c->stream));
+    AuditCall a;
+    a.kind = 1;
+    a.extent = c->n;
+    a.bits = d_bits;
+    a.region = d_region;
+    a.fit = d_fit;
+    c->last_audit = a;
+    return launch_rules(c, a);
+}
+
+int sparc_rules_queue_stats(void* ctx, uint64_t* out) {
+    Ctx* c = static_cast<Ctx*>(ctx);
+    if (!c || !out) return fail(c, SPARC_E_INVALID, "null argument");
+    out[0] = c->fq_cap;
+    out[1] = c->fq_last;
+    out[2] = c->fq_reruns;
+    return SPARC_OK;
 }
 
 int sparc_set_variant(void* ctx, int32_t which, int32_t value) {
@@ -2758,45 +2917,78 @@ int sparc_rules_finish(void* ctx, uint16_t* d_bits, uint64_t* d_fit) {
     int rc = check_ctx(c, false);
     if (rc) return rc;
     if (!c->rules) return fail(c, SPARC_E_STATE, "sparc_load_rules has not been called");
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (!c->h_count) HIPCHK(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_count), sizeof(uint32_t), hipHostMallocDefault));
+    auto read_count = [&](uint32_t& n) -> int {
+        HIPCHK(c, hipMemcpyAsync(c->h_count, c->fq_count, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        n = *c->h_count;
+        return SPARC_OK;
+    };
     uint32_t cnt = 0;
-    HIPCHK(c, hipMemcpy(&cnt, c->fq_count, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if ((rc = read_count(cnt))) return rc;
     if (cnt == 0) return SPARC_OK;
-    HIPCHK(c, hipMemset(c->fq_count, 0, sizeof(uint32_t)));
-    if (cnt > kFitQueueCap) {
-        char m[200];
-        snprintf(m, sizeof m, "%u exact-fit searches passed the node cap in one audit call (at most %u are finished on "
-                 "the host): raise the cap with sparc_set_rule_limits", cnt, kFitQueueCap);
-        return fail(c, SPARC_E_STATE, m);
+    const AuditCall a = c->last_audit;
+    if (a.kind == 0) return fail(c, SPARC_E_STATE, "queued exact-fit searches without a recorded audit call");
+    if (!d_bits || d_bits != a.bits) return fail(c, SPARC_E_STATE, "sparc_rules_finish: not the last audit call's bits");
+    if (cnt > c->fq_cap) {
+        // the queue overflowed: a larger queue, and the call again from where it started (an
+        // audit is deterministic: the same searches are queued, and the memo holds final answers)
+        if (a.kind == 2 && r1r_rollout(c)) return fail(c, SPARC_E_STATE, "queue overflow of a rule rollout without a snapshot");
+        uint64_t cap = c->fq_cap;
+        while (cap < cnt) cap *= 2;
+        HIPCHK(c, hipFree(c->fq_items));
+        c->fq_items = nullptr;
+        c->fq_cap = 0;
+        HIPCHK(c, hipMalloc(&c->fq_items, sizeof(FitTodo) * cap));
+        c->fq_cap = (uint32_t)std::min<uint64_t>(cap, 0xFFFFFFFFull);
+        if (a.kind == 2 && (rc = snapshot(c, a.stats, false))) return rc;
+        HIPCHK(c, hipMemsetAsync(c->fq_count, 0, sizeof(uint32_t), c->stream));
+        if ((rc = launch_rules(c, a))) return rc;
+        ++c->fq_reruns;
+        if ((rc = read_count(cnt))) return rc;
+        if (cnt > c->fq_cap) return fail(c, SPARC_E_STATE, "exact-fit queue overflow on the re-run");
     }
-    if (!d_bits) return fail(c, SPARC_E_INVALID, "null rule bits: the audit's pending exact fits need them");
     std::vector<FitTodo> todo(cnt);
     HIPCHK(c, hipMemcpy(todo.data(), c->fq_items, sizeof(FitTodo) * cnt, hipMemcpyDeviceToHost));
+    c->fq_last = cnt;
+    for (const FitTodo& it : todo)
+        if (it.pos >= a.extent || it.q >= c->num_puzzles)
+            return fail(c, SPARC_E_STATE, "exact-fit queue entry outside the last audit call");
+    // each distinct (puzzle, region cells) search once, on up to 16 host threads
+    std::vector<std::pair<uint32_t, uint64_t>> keys(cnt);
+    for (uint32_t k = 0; k < cnt; ++k) keys[k] = {todo[k].q, todo[k].rm};
+    std::sort(keys.begin(), keys.end());
+    keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+    std::vector<int8_t> res(keys.size(), 0);
+    parallel_for(keys.size(), [&](size_t k) { res[k] = (int8_t)host_fit(c, keys[k].first, keys[k].second); });
+    auto fits = [&](uint32_t q, uint64_t rm) {
+        const auto it = std::lower_bound(keys.begin(), keys.end(), std::make_pair(q, rm));
+        return res[(size_t)(it - keys.begin())] == 1;
+    };
     // per output entry: every queued region's answer (all must fit for poly_ylop_area), and the
     // fit mask of the regions that do
-    std::sort(todo.begin(), todo.end(), [](const FitTodo& a, const FitTodo& b) { return a.pos < b.pos; });
+    std::sort(todo.begin(), todo.end(), [](const FitTodo& x, const FitTodo& y) { return x.pos < y.pos; });
+    std::vector<RulePatch> patch;
     for (size_t k = 0; k < todo.size();) {
-        const uint64_t pos = todo[k].pos;
+        RulePatch r{todo[k].pos, 0ull, SPARC_RULE_SEARCH_EXHAUSTED, 0u};
         bool ok = true;
-        uint64_t fm = 0;
-        for (; k < todo.size() && todo[k].pos == pos; ++k) {
-            const int r = host_fit(c, todo[k].q, todo[k].rm);
-            ok &= r == 1;
-            if (r == 1) fm |= 1ull << (todo[k].rid & 63u);
+        for (; k < todo.size() && todo[k].pos == r.pos; ++k) {
+            const bool f = fits(todo[k].q, todo[k].rm);
+            ok &= f;
+            if (f) r.fit_or |= 1ull << (todo[k].rid & 63u);
         }
-        uint16_t b = 0;
-        HIPCHK(c, hipMemcpy(&b, d_bits + pos, sizeof b, hipMemcpyDeviceToHost));
-        b = (uint16_t)(b & ~SPARC_RULE_SEARCH_EXHAUSTED);
-        if (!ok) b = (uint16_t)(b & ~(SPARC_RULE_POLY_YLOP | SPARC_RULE_ALL));
-        HIPCHK(c, hipMemcpy(d_bits + pos, &b, sizeof b, hipMemcpyHostToDevice));
-        if (d_fit && fm) {
-            uint64_t f = 0;
-            HIPCHK(c, hipMemcpy(&f, d_fit + pos, sizeof f, hipMemcpyDeviceToHost));
-            f |= fm;
-            HIPCHK(c, hipMemcpy(d_fit + pos, &f, sizeof f, hipMemcpyHostToDevice));
-        }
+        if (!ok) r.clear |= SPARC_RULE_POLY_YLOP | SPARC_RULE_ALL;
+        patch.push_back(r);
     }
-    return SPARC_OK;
+    RulePatch* d_patch = nullptr;
+    HIPCHK(c, hipMalloc(&d_patch, sizeof(RulePatch) * patch.size()));
+    HIPCHK(c, hipMemcpyAsync(d_patch, patch.data(), sizeof(RulePatch) * patch.size(), hipMemcpyHostToDevice, c->stream));
+    k_rule_patch<<<grid_for(patch.size()), kBlock, 0, c->stream>>>(d_patch, (uint32_t)patch.size(), d_bits, d_fit);
+    rc = launch_check(c);
+    HIPCHK(c, hipMemsetAsync(c->fq_count, 0, sizeof(uint32_t), c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipFree(d_patch));
+    return rc;
 }
 
 int sparc_rules_host(void* ctx, uint16_t* bits, uint8_t* region, uint64_t* fit) {

@@ -34,7 +34,7 @@
 
 namespace sparc {
 
-constexpr uint32_t kErrRuleTable = 8;
+constexpr uint32_t kErrRuleTable = 8, kErrJoin = 16;   // Params::err bits (sparc_sync)
 // rule-plane indices of include/sparc_gym_amd.h (SPARC_RULE_PLANES), then the planes the loader
 // (sparc_load_rules) derives from the instance list for the device copy: the net instance area
 // of each cell (Σ poly areas − Σ ylop areas of the instances there, 8-bit two's complement,
@@ -48,9 +48,15 @@ enum : uint32_t {
 };
 constexpr int kAreaPlanes = 8;
 constexpr int kFitCells = 64;     // cell grid of the exact fit (15 x 15 lattice: 7 x 7 = 49)
-constexpr int kFitYlops = 16;     // per puzzle limits, validated by the loader
+// The GPU's search keeps its per-region lists in registers / scratch of these sizes; a puzzle with
+// more ylops or distinct poly shapes (instances sit at cell centres, one per cell, so never more
+// than 64 of either) is flagged by the loader (kHostFit) and its searches run on the host
+// (exact_fit<..., kHostFitMax, kHostFitMax, kHostFitPlanes>, sparc_kernels.hip host_fit)
+constexpr int kFitYlops = 16;
 constexpr int kFitShapes = 16;
 constexpr int kFitDepth = 64;
+constexpr int kHostFitMax = 64, kHostFitPlanes = 8;   // every valid puzzle: <= 64 cells, counts >= -65
+constexpr uint32_t kHostFit = 0x80000000u;            // instance count flag: searches on the host
 // default node cap of one exact-fit search on the GPU (sparc_set_fit_cap): a search that passes it
 // stops, and the host finishes it without a cap (FitQueue below, the C ABI's fallback), so
 // callers see the reference's unbounded answer
@@ -76,9 +82,9 @@ __device__ __forceinline__ void fit_queue_push(const FitQueue& fq, uint64_t pos,
 
 struct RulesTab {
     const uint64_t* __restrict__ planes;      // [P][RP_COUNT][W]
-    const uint32_t* __restrict__ inst_range;  // [P] first | count << 16
-    const uint32_t* __restrict__ inst;        // bit | ylop << 10 | cx << 11 | cy << 14 | shape << 17
-    const uint32_t* __restrict__ shape_range; // [S] first offset | count << 16
+    const uint2* __restrict__ inst_fc;        // [P] {first, count | kHostFit} into inst
+    const uint32_t* __restrict__ inst;        // bit | ylop << 10 | shape << 11
+    const uint2* __restrict__ shape_range;    // [S] {first offset, count} into shape_off
     const int32_t* __restrict__ shape_area;   // [S] sum of the shape array (the area of 722-723)
     const int8_t* __restrict__ shape_off;     // [offsets][2] (dcx, dcy) in cell units
     uint32_t num_puzzles;
@@ -92,9 +98,9 @@ struct RulesTab {
     const uint32_t* __restrict__ reg_tab;
     FitQueue fq;   // count null: no queue (region-table builds: the host scans the table instead)
     // [P][rule_row_u64<W>()]: what an audit reads when its env changes puzzle, in one contiguous
-    // record (puzzle_rules): the kBasePlanes planes, then reg_off | inst_range << 32, then the
-    // puzzle's info words x | y << 32 (W = 1: 96 B; the planes alone are spread over 264 B of the
-    // plane table)
+    // record (puzzle_rules): the kBasePlanes planes, then reg_off | inst first << 32, then the
+    // puzzle's info words x | y << 32 with y's bits 24-31 = instance count | host-fit flag << 7
+    // (W = 1: 96 B; the planes alone are spread over 264 B of the plane table)
     const uint64_t* __restrict__ rows;
 };
 template <int W>
@@ -143,40 +149,44 @@ struct BB {
 // scratch memory on every region)
 struct FitIn {
     const uint32_t* inst;
-    const uint32_t* shape_range;
+    const uint2* shape_range;
     const int8_t* shape_off;
     uint32_t first, count;   // the puzzle's instance range
     uint32_t CX, CY;         // cell grid
-    uint32_t cap;            // search nodes before the search is handed to the host
+    uint32_t cap;            // search nodes before the search is handed to the host (0: kHostFit)
 };
-__host__ __device__ __forceinline__ FitIn fit_in(const RulesTab& rt, uint32_t ir, uint32_t X, uint32_t Y) {
-    return FitIn{rt.inst, rt.shape_range, rt.shape_off, ir & 0xFFFFu, ir >> 16, (X - 1) / 2, (Y - 1) / 2, rt.fit_cap};
+// cf = count | kHostFit: a flagged puzzle's searches are never run on the GPU (cap 0)
+__host__ __device__ __forceinline__ FitIn fit_in(const RulesTab& rt, uint32_t first, uint32_t cf, uint32_t X,
+                                                 uint32_t Y) {
+    return FitIn{rt.inst, rt.shape_range, rt.shape_off, first, cf & ~kHostFit, (X - 1) / 2, (Y - 1) / 2,
+                 (cf & kHostFit) ? 0u : rt.fit_cap};
 }
 
 // ---------------------------------------------------------------- exact fit (736-838)
 // The search runs on the cell grid (CX x CY <= 7 x 7 cells, bit cx*CY + cy of a u64: the
 // reference's row-major order, so "the first negative cell" is the lowest set bit).  Cell
 // counts are two's-complement bit-sliced counters (kFitPlanes planes, -32..31 >= -(1 + 16
-// ylops)); placing a shape adds or subtracts its cell mask with a ripple over the planes.  A
+// ylops); the host's kHostFitPlanes: -128..127); placing a shape adds or subtracts its cell mask with a ripple over the planes.  A
 // shape is its cell pattern relative to its anchor (the shape's first cell in row-major order,
 // _get_offsets 840-855) plus the set of anchors at which it fits the grid (_try_place_polys
 // 858-871).
 constexpr int kFitPlanes = 6;
+template <int NP = kFitPlanes>
 struct FitGrid {
-    uint64_t p[kFitPlanes];
+    uint64_t p[NP];
     __host__ __device__ __forceinline__ void add(uint64_t m) {
 #pragma unroll
-        for (int i = 0; i < kFitPlanes; ++i) { const uint64_t t = p[i] & m; p[i] ^= m; m = t; }
+        for (int i = 0; i < NP; ++i) { const uint64_t t = p[i] & m; p[i] ^= m; m = t; }
     }
     __host__ __device__ __forceinline__ void sub(uint64_t m) {
 #pragma unroll
-        for (int i = 0; i < kFitPlanes; ++i) { const uint64_t t = ~p[i] & m; p[i] ^= m; m = t; }
+        for (int i = 0; i < NP; ++i) { const uint64_t t = ~p[i] & m; p[i] ^= m; m = t; }
     }
-    __host__ __device__ __forceinline__ uint64_t neg() const { return p[kFitPlanes - 1]; }
+    __host__ __device__ __forceinline__ uint64_t neg() const { return p[NP - 1]; }
     __host__ __device__ __forceinline__ uint64_t nonzero() const {
         uint64_t a = 0;
 #pragma unroll
-        for (int i = 0; i < kFitPlanes; ++i) a |= p[i];
+        for (int i = 0; i < NP; ++i) a |= p[i];
         return a;
     }
 };
@@ -184,8 +194,8 @@ struct FitGrid {
 // pattern (relative to the anchor) and fitting anchors of shape `sh` on a CX x CY cell grid
 __host__ __device__ __forceinline__ void fit_shape(const FitIn& rt, uint32_t sh, uint32_t CX, uint32_t CY, uint64_t& pat,
                                           uint64_t& va) {
-    const uint32_t sr = rt.shape_range[sh];
-    const uint32_t o0 = sr & 0xFFFFu, n = sr >> 16;
+    const uint2 sr = rt.shape_range[sh];
+    const uint32_t o0 = sr.x, n = sr.y;
     int mdx = 0, mdy0 = 0, mdy1 = 0;
     pat = 0;
     bool ok = true;
@@ -249,20 +259,24 @@ __device__ __forceinline__ uint64_t cell_mask_p8(const FitIn& in, uint64_t rc) {
 // 0 (does not fit) or -1: the search passed `cap` nodes without an answer (on the GPU the audit
 // then queues the region for the host, which runs this same function without a cap: the
 // reference's search is unbounded).  rm: the region's cells (cell_mask).
-template <int W, class I = uint32_t>
+//   NY, ND, PLANES: list sizes and counter planes (the GPU's; the host runs the puzzles the
+// loader flagged kHostFit with kHostFitMax / kHostFitPlanes).  cap == 0: -1 at once (a flagged
+// puzzle on the GPU).
+template <int W, class I = uint32_t, int NY = kFitYlops, int ND = kFitShapes, int PLANES = kFitPlanes>
 __host__ __device__ __noinline__ int exact_fit(const FitIn in, const BB<W> Rc, uint64_t rm, I cap) {
+    if (cap == 0) return -1;
     const FitIn& rt = in;
     const uint32_t CX = in.CX, CY = in.CY;
-    FitGrid g;
+    FitGrid<PLANES> g;
 #pragma unroll
-    for (int i = 0; i < kFitPlanes; ++i) g.p[i] = rm;    // -1 on the region
-    uint32_t ysh[kFitYlops], dsh[kFitShapes];
-    int cnt[kFitShapes];
+    for (int i = 0; i < PLANES; ++i) g.p[i] = rm;    // -1 on the region
+    uint32_t ysh[NY], dsh[ND];
+    int cnt[ND];
     int ny = 0, nd = 0, np = 0;
     for (uint32_t k = 0; k < in.count; ++k) {
         const uint32_t e = rt.inst[in.first + k];
         if (!Rc.test(e & 0x3FFu)) continue;
-        const uint32_t sh = e >> 17;
+        const uint32_t sh = e >> 11;
         if ((e >> 10) & 1u) {                 // ylop, kept sorted by shape (insertion sort)
             int j = ny++;
             while (j > 0 && ysh[j - 1] > sh) { ysh[j] = ysh[j - 1]; --j; }
@@ -275,10 +289,10 @@ __host__ __device__ __noinline__ int exact_fit(const FitIn in, const BB<W> Rc, u
             ++np;
         }
     }
-    uint64_t ypat[kFitYlops], yva[kFitYlops], dpat[kFitShapes], dva[kFitShapes];
+    uint64_t ypat[NY], yva[NY], dpat[ND], dva[ND];
     for (int k = 0; k < ny; ++k) fit_shape(rt, ysh[k], CX, CY, ypat[k], yva[k]);
     for (int k = 0; k < nd; ++k) fit_shape(rt, dsh[k], CX, CY, dpat[k], dva[k]);
-    int cur[kFitYlops + kFitDepth + 1];
+    int cur[NY + kFitDepth + 1];
     int pat[kFitDepth + 1];
     const int LMAX = ny + np;
     int L = 0;
@@ -399,7 +413,7 @@ __device__ __forceinline__ bool region_net_area(const RulesTab& rt, const FitIn&
         const uint32_t e = rt.inst[fin.first + k];
         if (!Rc.test(e & 0x3FFu)) continue;
         has = true;
-        const int a = rt.shape_area[e >> 17];
+        const int a = rt.shape_area[e >> 11];
         net += ((e >> 10) & 1u) ? -a : a;
     }
     return has;
@@ -459,8 +473,8 @@ template <int W>
 __device__ uint32_t region_table_word(const Params& p, const RulesTab& rt, uint32_t q, uint32_t g) {
     const uint4 inf = p.tab.info[q];
     const uint32_t X = inf.x & 0xFFu, Y = (inf.x >> 8) & 0xFFu;
-    const uint32_t ir = rt.inst_range[q];
-    const FitIn fin = fit_in(rt, ir, X, Y);
+    const uint2 fc = rt.inst_fc[q];
+    const FitIn fin = fit_in(rt, fc.x, fc.y, X, Y);
     const uint32_t cells = fin.CX * fin.CY;
     BB<W> pl[RP_ABI];
     const uint64_t* gp = rt.planes + (size_t)q * RP_COUNT * W;
@@ -506,13 +520,13 @@ __device__ __forceinline__ PuzzleRules<W> puzzle_rules(const Params& p, const Ru
     const uint64_t m0 = g[10 * W], m1 = g[10 * W + 1];
     const uint32_t ix = (uint32_t)m1, iy = (uint32_t)(m1 >> 32);
     const uint32_t X = ix & 0xFFu, Y = (ix >> 8) & 0xFFu;
-    const uint32_t ir = (uint32_t)(m0 >> 32);
     r.q = q;
     r.fo = (uint32_t)m0;
     r.tx = iy & 0xFFu;
     r.ty = (iy >> 8) & 0xFFu;
     r.tbit = r.tx * p.pitch + r.ty;
-    r.fin = fit_in(rt, ir, X, Y);
+    const uint32_t cf = ((iy >> 24) & 0x7Fu) | ((iy >> 31) ? kHostFit : 0u);
+    r.fin = fit_in(rt, (uint32_t)(m0 >> 32), cf, X, Y);
     return r;
 }
 

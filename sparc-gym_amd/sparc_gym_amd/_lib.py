@@ -35,8 +35,8 @@ class SparcStateHost(ctypes.Structure):
 
 class SparcRulesTable(ctypes.Structure):
     _fields_ = [("num_puzzles", ctypes.c_int32), ("num_inst", ctypes.c_int32), ("num_shapes", ctypes.c_int32),
-                ("num_offsets", ctypes.c_int32), ("planes", c_void_p), ("inst_range", c_void_p), ("inst", c_void_p),
-                ("shape_range", c_void_p), ("shape_area", c_void_p), ("shape_off", c_void_p)]
+                ("num_offsets", ctypes.c_int32), ("planes", c_void_p), ("inst_first", c_void_p), ("inst", c_void_p),
+                ("shape_first", c_void_p), ("shape_area", c_void_p), ("shape_off", c_void_p)]
 
 
 _SIGS = {
@@ -75,6 +75,7 @@ _SIGS = {
     "sparc_rules_finish": ([c_void_p, c_void_p, c_void_p], c_int32),
     "sparc_set_rule_limits": ([c_void_p, ctypes.c_uint32, c_uint64], c_int32),
     "sparc_set_variant": ([c_void_p, c_int32, c_int32], c_int32),
+    "sparc_rules_queue_stats": ([c_void_p, c_void_p], c_int32),
     "sparc_comm_unique_id": ([c_void_p], c_int32),
     "sparc_comm_init": ([c_void_p, c_int32, c_int32, c_void_p, ctypes.POINTER(c_void_p)], c_int32),
     "sparc_comm_destroy": ([c_void_p], c_int32),
@@ -90,12 +91,13 @@ class SparcError(RuntimeError):
     pass
 
 
-def load(path=None):
+def load(path=None, any_abi=False):
     """Load and type the HIP library (cached).  Raises if it is missing: no CPU fallback.
 
     The product path always loads the in-tree build (``path=None``).  Profiling tools may load
-    another build of the same ABI by calling ``load(path)`` themselves before any env is
-    created; later ``load()`` calls then return that library."""
+    another build by calling ``load(path)`` themselves before any env is created; later
+    ``load()`` calls then return that library.  ``any_abi``: an A/B build of an earlier ABI
+    version (the rollout entry points are unchanged; symbols it lacks stay unbound)."""
     global _lib
     if _lib is not None:
         if path is not None and os.path.abspath(path) != _lib._sparc_path:
@@ -106,10 +108,12 @@ def load(path=None):
         raise ImportError(f"{path} not found: build the HIP extension (make -C sparc-gym_amd)")
     lib = ctypes.CDLL(path)
     for name, (args, res) in _SIGS.items():
+        if any_abi and not hasattr(lib, name):
+            continue
         f = getattr(lib, name)
         f.argtypes = args
         f.restype = res
-    if lib.sparc_abi_version() != 1:
+    if lib.sparc_abi_version() != 2 and not any_abi:
         raise ImportError("libsparc_gym_amd ABI version mismatch")
     lib._sparc_path = os.path.abspath(path)
     _lib = lib

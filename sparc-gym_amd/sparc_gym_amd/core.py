@@ -51,13 +51,13 @@ class SparcCore:
     def load_rules(self, rt: RulesTable):
         """Upload the rule-audit table (puzzles.pack_rules) for the loaded puzzles."""
         planes = np.ascontiguousarray(rt.planes, np.uint64)
-        rng = np.ascontiguousarray(rt.inst_range, np.uint32)
+        first = np.ascontiguousarray(rt.inst_first, np.uint32)
         inst = np.ascontiguousarray(rt.inst, np.uint32)
-        sr = np.ascontiguousarray(rt.shape_range, np.uint32)
+        sf = np.ascontiguousarray(rt.shape_first, np.uint32)
         sa = np.ascontiguousarray(rt.shape_area, np.int32)
         so = np.ascontiguousarray(rt.shape_off, np.int8)
-        t = _lib.SparcRulesTable(len(rng), len(inst), len(sr), len(so), planes.ctypes.data, rng.ctypes.data,
-                                 inst.ctypes.data if len(inst) else None, sr.ctypes.data if len(sr) else None,
+        t = _lib.SparcRulesTable(len(first) - 1, len(inst), len(sa), len(so), planes.ctypes.data, first.ctypes.data,
+                                 inst.ctypes.data if len(inst) else None, sf.ctypes.data,
                                  sa.ctypes.data if len(sa) else None, so.ctypes.data if len(so) else None)
         self._check(self.lib.sparc_load_rules(self.ctx, ctypes.byref(t)))
         self.rules = rt
@@ -82,6 +82,13 @@ class SparcCore:
         """Finish, on the host and without a node cap, the exact-fit searches of the last audit
         call that passed the GPU's cap, and patch its bits (and fit) in place (synchronous)."""
         self._check(self.lib.sparc_rules_finish(self.ctx, d_bits, d_fit))
+
+    def rules_queue_stats(self):
+        """The exact-fit queue: capacity, searches the last rules_finish ran on the host, calls
+        run again after a queue overflow."""
+        out = np.zeros(3, np.uint64)
+        self._check(self.lib.sparc_rules_queue_stats(self.ctx, out.ctypes.data))
+        return {"capacity": int(out[0]), "last_searches": int(out[1]), "reruns": int(out[2])}
 
     def set_rule_limits(self, fit_cap=0, table_entries=0):
         """GPU node cap of one exact-fit search (0: 2^26) and the region-code table budget in

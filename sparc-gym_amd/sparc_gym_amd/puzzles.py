@@ -317,11 +317,18 @@ RULE_SKIP_LAYERS = ("visited", "gaps", "agent_location", "target_location")   # 
 class RulesTable:
     """Rule-audit table (layout: include/sparc_gym_amd.h, sparc_rules_table)."""
     planes: np.ndarray       # uint64 [P][RULE_PLANES][words]
-    inst_range: np.ndarray   # uint32 [P]
-    inst: np.ndarray         # uint32 [I]
-    shape_range: np.ndarray  # uint32 [S]
+    inst_first: np.ndarray   # uint32 [P + 1] offsets into inst
+    inst: np.ndarray         # uint32 [I]: bit | ylop << 10 | shape << 11
+    shape_first: np.ndarray  # uint32 [S + 1] offsets into shape_off
     shape_area: np.ndarray   # int32 [S]
     shape_off: np.ndarray    # int8 [O][2]
+
+    def inst_range(self, q):
+        """(first, count) of puzzle q's instances."""
+        return int(self.inst_first[q]), int(self.inst_first[q + 1]) - int(self.inst_first[q])
+
+    def shape_offsets(self, s):
+        return [(int(dx), int(dy)) for dx, dy in self.shape_off[int(self.shape_first[s]):int(self.shape_first[s + 1])]]
 
 
 def _bits_of(mask, pitch, words):
@@ -359,7 +366,7 @@ def pack_rules(puzzles, table: PuzzleTable) -> RulesTable:
     pitch, W = table.pitch, table.words
     P = len(puzzles)
     planes = np.zeros((P, RULE_PLANES, W), np.uint64)
-    inst_range = np.zeros(P, np.uint32)
+    inst_first = np.zeros(P + 1, np.uint64)
     inst, shapes, shape_ids = [], [], {}
     for q, p in enumerate(puzzles):
         X, Y = int(p["x_size"]), int(p["y_size"])
@@ -415,17 +422,17 @@ def pack_rules(puzzles, table: PuzzleTable) -> RulesTable:
                         shapes.append(key)
                     b = x * pitch + y
                     planes[q, RP_INST, b >> 6] |= np.uint64(1) << np.uint64(b & 63)
-                    inst.append(b | (int(ylop) << 10) | (((x - 1) // 2) << 11) | (((y - 1) // 2) << 14)
-                                | (shape_ids[key] << 17))
-        if len(inst) - first > 0xFFFF or first > 0xFFFF:
-            raise ValueError("too many poly/ylop instances for the rule table")
-        inst_range[q] = first | ((len(inst) - first) << 16)
-    offs, srange, sarea = [], [], []
+                    inst.append(b | (int(ylop) << 10) | (shape_ids[key] << 11))
+        inst_first[q + 1] = len(inst)
+    offs, sfirst, sarea = [], [0], []
     for o, area in shapes:
-        srange.append(len(offs) | (len(o) << 16))
         sarea.append(area)
         offs.extend(o)
-    if len(offs) > 0xFFFF or len(shapes) >= 1 << 15:
-        raise ValueError("too many polyshapes for the rule table")
-    return RulesTable(planes, inst_range, np.asarray(inst, np.uint32), np.asarray(srange, np.uint32),
-                      np.asarray(sarea, np.int32), np.asarray(offs, np.int8).reshape(-1, 2))
+        sfirst.append(len(offs))
+    if len(shapes) >= 1 << 21 or len(inst) >= 1 << 32 or len(offs) >= 1 << 32:
+        raise ValueError("rule table past 2^21 distinct polyshapes or 2^32 entries")
+    if any(not -128 <= v <= 127 for o, _ in shapes for d in o for v in d):
+        raise ValueError("polyshape wider than 127 cells")
+    return RulesTable(planes, inst_first.astype(np.uint32), np.asarray(inst, np.uint32),
+                      np.asarray(sfirst, np.uint32), np.asarray(sarea, np.int32),
+                      np.asarray(offs, np.int8).reshape(-1, 2))

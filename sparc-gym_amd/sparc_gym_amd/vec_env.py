@@ -202,7 +202,9 @@ class SPaRCVecEnv:
             out["fit"] = torch.empty(n, dtype=torch.int64, device=self.device)
         self.core.rules_device(self._rbits.data_ptr(), out["region"].data_ptr() if region else None,
                                out["fit"].data_ptr() if fit else None)
-        # exact fits that passed the GPU's node cap: finished on the host (a sync; no-op otherwise)
+        # exact fits that passed the GPU's node cap: finished on the host.  This synchronises the
+        # stream (a 4-byte read of the queue count when nothing was queued), so rule_audit() and
+        # step() with rules=True return final bits and are synchronous
         self.core.rules_finish(self._rbits.data_ptr(), out["fit"].data_ptr() if fit else None)
         return out
 

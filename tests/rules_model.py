@@ -22,7 +22,7 @@ def exact_fit(rt, first, count, Rc, pitch, CX, CY):
         e = int(rt.inst[first + k])
         if not (Rc >> (e & 0x3FF)) & 1:
             continue
-        sh = e >> 17
+        sh = e >> 11
         if (e >> 10) & 1:
             ysh.append(sh)
         elif sh in dsh:
@@ -34,9 +34,7 @@ def exact_fit(rt, first, count, Rc, pitch, CX, CY):
     ny, npoly = len(ysh), sum(cnt)
 
     def offs(sh):
-        sr = int(rt.shape_range[sh])
-        o0, n = sr & 0xFFFF, sr >> 16
-        return [(int(rt.shape_off[o0 + k][0]), int(rt.shape_off[o0 + k][1])) for k in range(n)]
+        return rt.shape_offsets(sh)
 
     def place(sh, a, sign):
         ax, ay = divmod(a, CY)
@@ -117,8 +115,7 @@ def audit(rt, table, q, vis, x, y):
     full = (1 << (64 * W)) - 1
     cells, lattice, gaps = pl[RP_CELLS], pl[RP_LATTICE], pl[RP_GAPS]
     allowed = (lattice & ~(gaps | vis) | cells) & full
-    ir = int(rt.inst_range[q])
-    first, count = ir & 0xFFFF, ir >> 16
+    first, count = rt.inst_range(q)
     sq_ok = star_ok = poly_ok = True
     fit_ok, rid, rmap = 0, 0, {}
     remaining = cells
@@ -151,7 +148,7 @@ def audit(rt, table, q, vis, x, y):
             e = int(rt.inst[first + k])
             if (Rc >> (e & 0x3FF)) & 1:
                 has = True
-                a = int(rt.shape_area[e >> 17])
+                a = int(rt.shape_area[e >> 11])
                 if (e >> 10) & 1:
                     ya += a
                 else:

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     lib = _lib.load()
     for name in declared_symbols():
         assert hasattr(lib, name), name
-    assert lib.sparc_abi_version() == 1
+    assert lib.sparc_abi_version() == 2
 
 
 def test_create_validates_before_touching_a_device():

@@ -211,19 +211,21 @@ def test_rollout_rule_bits_ragged_batches(on_gpu, n):
 
 
 def test_rollout_rules_c3r_full_size(on_gpu):
-    """The bench's c3r workload (bench.py --config c3r) through the bench's own C-ABI call
-    (sparc_rollout_rules_device: k_rollout1r on this pool): 65,536 envs of the c3 pool,
-    traceback, next-step autoreset, uint8 actions in HBM, the audit after every step, THREE
-    back-to-back 50-step launches with the state carried through HBM (50 = 4 tiles of 12 + a
-    partial tile of 2).  Reward codes, flags and stats equal the plain rollout's (the split
-    kernel, itself oracle-pinned); the rule bits of 256 sampled envs at every step of every
-    launch equal the oracle's audit (oracle/rules_ref.py) of the C oracle's state after that
-    step (SPaRC_Gym.py:941-950, 1227)."""
+    """The bench's c3r workload at the bench's launch shape (bench.py --config c3r): 65,536 envs of
+    the c3 pool, traceback, next-step autoreset, uint8 actions in HBM, the audit after every step,
+    TWO back-to-back 2,000-step launches through the bench's own C-ABI call
+    (sparc_rollout_rules_device: k_rollout1r on this pool, 200 tiles of its rings per launch) with
+    the state carried through HBM.  Reward codes, flags and stats equal the plain rollout's (the
+    split kernel, itself oracle-pinned); the rule bits of 256 sampled envs at 200 steps spread over
+    both launches (every step of the first and last tiles, the tile-ring wrap points RT - 1 / RT /
+    2 RT - 1 of a sample of tiles, the steps either side of the launch boundary, and random steps)
+    equal the oracle's audit (oracle/rules_ref.py) of the C oracle's state after that step
+    (SPaRC_Gym.py:941-950, 1227)."""
     from oracle import COracle
     from sparc_gym_amd import SPaRCVecEnv, synthetic
     from sparc_gym_amd.puzzles import process_puzzles
     proc = process_puzzles(synthetic.make_puzzles(1024, seed=0, sizes=((3, 3),), full_properties=True))
-    n, T, L = 65536, 50, 3
+    n, T, L, RT = 65536, 2000, 2, 10
     pids = (np.arange(n, dtype=np.uint64) * 2654435761 % 1024).astype(np.int64)
     kw = dict(processed=proc, traceback=True, autoreset="next_step", observation="compact", rules=True,
               max_steps=2000)
@@ -240,16 +242,24 @@ def test_rollout_rules_c3r_full_size(on_gpu):
     for k in range(L):   # bench.py run(): raw C-ABI calls on pre-validated buffers
         a.core.rollout_rules_device(T, acts[k].data_ptr(), rew[k].data_ptr(), flg[k].data_ptr(), sa.data_ptr(),
                                     bits[k].data_ptr())
+    a.core.sync()
     b = SPaRCVecEnv(n, **kw)
     b.reset(options={"puzzle_index": pids})
     sb = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
-    rb = b.rollout(L * T, acts.reshape(L * T, n), stats=sb)
-    assert torch.equal(rew.reshape(L * T, n), rb["reward_code"]) and torch.equal(flg.reshape(L * T, n), rb["flags"])
+    for k in range(L):
+        rb = b.rollout(T, acts[k], stats=sb)
+        assert torch.equal(rew[k], rb["reward_code"]) and torch.equal(flg[k], rb["flags"]), k
     assert torch.equal(sa, sb)
     bits = bits.reshape(L * T, n).cpu().numpy().astype(np.uint16)
     assert not (bits & (1 << 9)).any()
     rng = np.random.default_rng(2)
     idx = np.sort(rng.choice(n, 256, replace=False))
+    steps = set(range(RT)) | set(range(L * T - RT, L * T)) | {T - 2, T - 1, T, T + 1, T + RT - 1, T + RT}
+    for tile in rng.choice(L * T // RT, 40, replace=False):
+        steps |= {int(tile) * RT + RT - 1, int(tile) * RT + RT} - {L * T}
+    steps |= set(int(x) for x in rng.choice(L * T, 120, replace=False))
+    steps = sorted(steps)
+    assert len(steps) >= 200 and min(steps) == 0 and max(steps) == L * T - 1
     pool = [{"x_size": p["x_size"], "y_size": p["y_size"], "start": list(p["start_location"]),
              "target": list(p["target_location"]), "solution_count": p["solution_count"],
              "solution_paths": p["solution_paths"], "gaps": p["obs_array"]["gaps"]} for p in proc]
@@ -257,8 +267,10 @@ def test_rollout_rules_c3r_full_size(on_gpu):
     o = COracle(pool, len(idx), True, 2000, autoreset=1)
     o.reset(pids[idx])
     an = acts.reshape(L * T, n)[:, torch.from_numpy(idx).cuda()].cpu().numpy()
-    for t in range(L * T):
-        o.rollout(1, np.ascontiguousarray(an[t:t + 1]))
+    done = 0
+    for t in steps:
+        o.rollout(t + 1 - done, np.ascontiguousarray(an[done:t + 1]))
+        done = t + 1
         st = o.state()
         for j, i in enumerate(idx):
             p = refp[int(st["pid"][j])]

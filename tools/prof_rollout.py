@@ -33,7 +33,7 @@ import torch  # noqa: E402
 if a.lib:   # another build of the library, loaded (after torch's HIP runtime) before the package uses it
     torch.cuda.init()
     from sparc_gym_amd import _lib as _sparc_lib  # noqa: E402
-    _sparc_lib.load(os.path.abspath(a.lib))
+    _sparc_lib.load(os.path.abspath(a.lib), any_abi=True)
 
 from sparc_gym_amd import SPaRCVecEnv  # noqa: E402
 from sparc_gym_amd.puzzles import pack_table  # noqa: E402
