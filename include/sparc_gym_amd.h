@@ -314,8 +314,11 @@ int sparc_set_rule_limits(void *ctx, uint32_t fit_cap_nodes, uint64_t table_entr
  *                                      where k_rollout1r applies; 0: default
  *  SPARC_VARIANT_R1R_SHAPE             k_rollout1r's <G, A, RT>: 0 <2, 5, 10> (default),
  *                                      1 <4, 3, 12>, 2 <2, 4, 12>
+ *  SPARC_VARIANT_OBS_INLINE            1: sparc_rollout_obs_device on the per-wave kernel that
+ *                                      writes its own planes; 0: default (writer waves)
  * SPARC_E_INVALID for another `which` or value. */
-enum { SPARC_VARIANT_IO_CODES_OFF = 1, SPARC_VARIANT_RULE_ROLLOUT_GENERIC = 2, SPARC_VARIANT_R1R_SHAPE = 3 };
+enum { SPARC_VARIANT_IO_CODES_OFF = 1, SPARC_VARIANT_RULE_ROLLOUT_GENERIC = 2, SPARC_VARIANT_R1R_SHAPE = 3,
+       SPARC_VARIANT_OBS_INLINE = 4 };
 int sparc_set_variant(void *ctx, int32_t which, int32_t value);
 
 /* ---- multi-GPU: the end-of-batch gather over RCCL (xGMI) -------------------------------------

@@ -162,19 +162,39 @@ __device__ __forceinline__ void obs_build_lut(uint16_t* lut, uint32_t XD, uint32
     }
 }
 
-// the wave's envs [0, cnt) -> planes at vout / aout (run starts, entry `base` of the whole
-// array, for the alignment test); every lane of the wave must call this (wave-uniform)
+// this lane's env board and agent bit into the wave's staging area (kObsNone: no env)
 template <int W>
-__device__ __forceinline__ void obs_emit(ObsWave<W>* ow, const uint16_t* lut, uint32_t lane, bool has_env,
-                                         const uint64_t (&v)[W], uint32_t ab, uint32_t cnt, uint32_t XY,
-                                         int32_t* __restrict__ vout, int32_t* __restrict__ aout) {
+__device__ __forceinline__ void obs_stage(ObsWave<W>* ow, uint32_t lane, bool has_env, const uint64_t (&v)[W],
+                                          uint32_t ab) {
 #pragma unroll
     for (int k = 0; k < W; ++k) {
         ow->vis[2 * k][lane] = (uint32_t)v[k];
         ow->vis[2 * k + 1][lane] = (uint32_t)(v[k] >> 32);
     }
     ow->ab[lane] = has_env ? ab : (uint32_t)kObsNone;
+}
+
+// the staged envs [0, cnt) of ow -> planes at vout / aout (run starts); every lane of the
+// writing wave calls this (wave-uniform)
+template <int W>
+__device__ __forceinline__ void obs_write(const ObsWave<W>* ow, const uint16_t* lut, uint32_t lane, uint32_t cnt,
+                                          uint32_t XY, int32_t* __restrict__ vout, int32_t* __restrict__ aout);
+
+// the wave's envs [0, cnt) -> planes at vout / aout (run starts, entry `base` of the whole
+// array, for the alignment test); every lane of the wave must call this (wave-uniform)
+template <int W>
+__device__ __forceinline__ void obs_emit(ObsWave<W>* ow, const uint16_t* lut, uint32_t lane, bool has_env,
+                                         const uint64_t (&v)[W], uint32_t ab, uint32_t cnt, uint32_t XY,
+                                         int32_t* __restrict__ vout, int32_t* __restrict__ aout) {
+    obs_stage<W>(ow, lane, has_env, v, ab);
     wave_lds_fence();
+    obs_write<W>(ow, lut, lane, cnt, XY, vout, aout);
+    wave_lds_fence();
+}
+
+template <int W>
+__device__ __forceinline__ void obs_write(const ObsWave<W>* ow, const uint16_t* lut, uint32_t lane, uint32_t cnt,
+                                          uint32_t XY, int32_t* __restrict__ vout, int32_t* __restrict__ aout) {
     const uint32_t total = cnt * XY;
     // 16-B stores need both runs 16-B aligned (true whenever N * XY % 4 == 0)
     const bool vec = (((reinterpret_cast<uintptr_t>(vout) | reinterpret_cast<uintptr_t>(aout)) & 15u) == 0);
@@ -215,7 +235,6 @@ __device__ __forceinline__ void obs_emit(ObsWave<W>* ow, const uint16_t* lut, ui
             ++l;
         }
     }
-    wave_lds_fence();
 }
 
 // step() + the 'new' observation in one launch (SPaRCVecEnv.step): the gym one-call-per-step
@@ -536,6 +555,93 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
         s.z += acc.z;
         s.w += acc.w;
         stats[i] = s;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Rollout with the 'new' observation planes after every step (config c4: ~1 KB of plane stores per
+// env-step), the planes written by a WRITER wave.  vmcnt counts loads and stores in issue order,
+// so a wave that both gathers trie records and stores planes (k_rollout<..., OBS>) waits, at each
+// step's record wait, for every plane store it issued in the step before: its stores drain in
+// bursts (MI355X, c4: 62-78 % of 8 TB/s, 0.71 of the box's fill_ bandwidth).  Here a workgroup of
+// 256 envs has 4 compute waves (Env<W>, one lane per env) and one writer wave: in iteration t the
+// compute waves run step t and stage each env's board and agent bit in LDS buffer t % 2
+// (obs_stage), while the writer streams the planes of step t - 1 from the other buffer
+// (obs_write: 16-B pieces of each 64-env run, every store instruction 1 KB of contiguous memory);
+// one barrier per step hands the buffers over.  The writer issues no load and never waits for its
+// stores; the compute waves' own stores are a byte of reward code and of flags per env-step.
+constexpr int kBlockOw = 320;
+template <int W, bool TB>
+__host__ __device__ constexpr size_t obsw_lds_bytes() {
+    return 8 * sizeof(ObsWave<W>) + kObsCells * sizeof(uint16_t) + ((W == 1 && TB) ? 4 * 64 * 64 : 0);
+}
+template <int W, bool TB, bool RAND>
+__global__ void __launch_bounds__(kBlockOw) __attribute__((amdgpu_waves_per_eu(5)))
+    k_rollout_obsw(Params p, int32_t T, const uint8_t* __restrict__ act, uint64_t seed, uint64_t t0,
+                   int8_t* __restrict__ rew, uint8_t* __restrict__ flg, int4* __restrict__ stats, ObsTrace ot) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    ObsWave<W>* ob = reinterpret_cast<ObsWave<W>*>(smem);   // [2 buffers][4 compute waves]
+    uint16_t* lut = reinterpret_cast<uint16_t*>(smem + 8 * sizeof(ObsWave<W>));
+    obs_build_lut(lut, ot.XD, ot.YD, p.pitch, W, threadIdx.x, kBlockOw);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const size_t n = p.n;
+    const uint32_t XY = ot.XD * ot.YD;
+    if (wv == 4) {                                               // ---- the writer wave
+        for (int32_t t = 0; t <= T; ++t) {
+            if (t > 0) {
+                for (uint32_t k = 0; k < 4; ++k) {
+                    const size_t wb = (size_t)blockIdx.x * 256u + k * 64u;
+                    if (wb >= n) break;
+                    const uint32_t cnt = n - wb < 64u ? (uint32_t)(n - wb) : 64u;
+                    const size_t run = ((size_t)(t - 1) * n + wb) * XY;
+                    obs_write<W>(ob + ((t - 1) & 1) * 4 + k, lut, lane, cnt, XY, ot.vout ? ot.vout + run : nullptr,
+                                 ot.aout ? ot.aout + run : nullptr);
+                }
+            }
+            __syncthreads();                                     // B_t
+        }
+        return;
+    }
+    const uint32_t i = blockIdx.x * 256u + wv * 64u + lane;     // ---- compute waves
+    const bool active = i < n;
+    const PuzzleSrc<W> src{p.tab.info, p.tab.root, p.tab.open, p.tab.init, p.tab.row1};
+    using Stack = typename std::conditional<(W == 1 && TB), LdsStack<64>, RegStack>::type;
+    Env<W, TB, Stack> e;
+    if constexpr (W == 1 && TB) e.stk.col = smem + 8 * sizeof(ObsWave<W>) + kObsCells * sizeof(uint16_t) + wv * 64 * 64 + lane;
+    if (active) e.load(p, src, i);
+    int4 acc = make_int4(0, 0, 0, 0);
+    const uint64_t gid = p.env_offset + i;
+    for (int32_t t = 0; t < T; ++t) {
+        uint64_t v[W];
+#pragma unroll
+        for (int k = 0; k < W; ++k) v[k] = 0;
+        uint32_t ab = 0;
+        if (active) {
+            const uint32_t a = RAND ? uint_rand_action(seed, gid, t0 + (uint64_t)t) : act[(size_t)t * n + i];
+            uint32_t f;
+            const int code = e.advance(p, src, a, f);
+            if (rew) rew[(size_t)t * n + i] = (int8_t)code;
+            if (flg) flg[(size_t)t * n + i] = (uint8_t)f;
+            acc.x += code;
+            acc.y += (f & 3u) ? 1 : 0;
+            acc.z += ((f & 3u) && code == 100) ? 1 : 0;
+            acc.w += (f & 64u) ? 1 : 0;
+            e.obs_words(p, src, v, ab);
+        }
+        obs_stage<W>(ob + (t & 1) * 4 + wv, lane, active, v, ab);
+        __syncthreads();                                         // B_t
+    }
+    __syncthreads();                                             // B_T: the writer's last step
+    if (!active) return;
+    e.store(p, src, i);
+    if (stats) {
+        int4 st = stats[i];
+        st.x += acc.x;
+        st.y += acc.y;
+        st.z += acc.z;
+        st.w += acc.w;
+        stats[i] = st;
     }
 }
 
@@ -1635,6 +1741,7 @@ struct Ctx {
     bool rules_generic = false;   // rule rollouts on k_rollout<..., RULES>
     bool io_codes_off = false;    // k_rollout1s / k_rolloutWs keep the reward codes on the trie wave
     int r1r_shape = 0;            // k_rollout1r's <G, A, RT> (0: <2, 5, 10>; 1, 2: A/B, tests)
+    bool obs_inline = false;      // 'new'-plane rollouts on k_rollout<..., OBS> instead of k_rollout_obsw
     // exact-fit searches past the GPU's node cap (sparc_set_fit_cap) are finished on the host
     // from these copies of the rule table (sparc_rules.hpp exact_fit, the same code)
     uint32_t fit_cap = kFitCap;
@@ -2451,6 +2558,23 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
         t0 += (uint64_t)T16;
         T -= T16;
     }
+    if (ot && !c->obs_inline) {
+        // the 'new' planes by writer waves (k_rollout_obsw): 256-env workgroups, one barrier per step
+        dispatch_w_tb(c->W, c->cfg.traceback, [&](auto w, auto tb) {
+            constexpr int W = decltype(w)::value;
+            constexpr bool TB = decltype(tb)::value;
+            const size_t shm = obsw_lds_bytes<W, TB>();
+            const dim3 g((unsigned)((c->n + 255) / 256));
+            auto launch = [&](auto kern, const uint8_t* a) {
+                if (shm > 64 * 1024 && (lds_rc = allow_big_lds(c, reinterpret_cast<const void*>(kern)))) return;
+                kern<<<g, kBlockOw, shm, c->stream>>>(p, T, a, seed, t0, d_rew, d_flags, st, *ot);
+            };
+            if (d_act) launch(k_rollout_obsw<W, TB, false>, d_act);
+            else launch(k_rollout_obsw<W, TB, true>, nullptr);
+        });
+        if (lds_rc) return lds_rc;
+        return launch_check(c);
+    }
     dispatch_w_tb(c->W, c->cfg.traceback, [&](auto w, auto tb) {
         constexpr int W = decltype(w)::value;
         constexpr bool TB = decltype(tb)::value;
@@ -2895,6 +3019,10 @@ int sparc_set_variant(void* ctx, int32_t which, int32_t value) {
         case SPARC_VARIANT_R1R_SHAPE:
             if (value < 0 || value > 2) break;
             c->r1r_shape = value;
+            return SPARC_OK;
+        case SPARC_VARIANT_OBS_INLINE:
+            if (value != 0 && value != 1) break;
+            c->obs_inline = value == 1;
             return SPARC_OK;
         default:
             return fail(c, SPARC_E_INVALID, "unknown variant");

@@ -96,7 +96,7 @@ class SparcCore:
         self._check(self.lib.sparc_set_rule_limits(self.ctx, int(fit_cap or 0), int(table_entries or 0)))
 
     # sparc_set_variant (include/sparc_gym_amd.h): kernel variants with identical results
-    VARIANT_IO_CODES_OFF, VARIANT_RULE_ROLLOUT_GENERIC, VARIANT_R1R_SHAPE = 1, 2, 3
+    VARIANT_IO_CODES_OFF, VARIANT_RULE_ROLLOUT_GENERIC, VARIANT_R1R_SHAPE, VARIANT_OBS_INLINE = 1, 2, 3, 4
 
     def set_variant(self, which, value):
         """Debug: select a kernel variant of identical results for this context (A/B, tests)."""

@@ -565,3 +565,34 @@ def test_step_gym_action_types_and_outputs(on_gpu):
         v.step(torch.zeros(n, dtype=torch.float32))
     with pytest.raises(ValueError):
         v.core.step_gym_device(torch.zeros(n, dtype=torch.int16, device="cuda").data_ptr(), 2)
+
+
+@pytest.mark.parametrize("name,tb,n", [("mixed_5_11", True, 4096), ("7x7_full", False, 1001), ("15x15", True, 300)])
+def test_rollout_obs_writer_waves_equal_inline(on_gpu, name, tb, n):
+    """rollout(obs=True) runs k_rollout_obsw (compute waves stage the boards, a writer wave per
+    256 envs streams the planes); the per-wave kernel that writes its own planes
+    (sparc_set_variant SPARC_VARIANT_OBS_INLINE) gives identical planes, codes, flags, stats and
+    state, with file actions and with the in-kernel random actions, over two launches."""
+    from sparc_gym_amd import SPaRCVecEnv
+    proc, table = _make(name, seed=23 + n)
+    rng = np.random.default_rng(n)
+    pids = rng.integers(len(proc), size=n)
+    acts = torch.from_numpy(rng.integers(0, 5, size=(40, n)).astype(np.uint8)).cuda()
+    runs = []
+    for inline in (False, True):
+        v = SPaRCVecEnv(n, processed=proc, table=table, traceback=tb, max_steps=30, observation="new")
+        if inline:
+            v.core.set_variant(v.core.VARIANT_OBS_INLINE, 1)
+        v.reset(options={"puzzle_index": pids})
+        st = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
+        r1 = v.rollout(24, acts[:24].contiguous(), obs=True, stats=st)
+        r2 = v.rollout(16, None, seed=5, t0=24, obs=True, stats=st)
+        runs.append(([r[k].cpu().numpy() for r in (r1, r2) for k in ("reward_code", "flags", "visited",
+                                                                        "agent_location")],
+                     st.cpu().numpy(), v.state()))
+    (a, sa, xa), (b, sb, xb) = runs
+    for u, w in zip(a, b):
+        assert np.array_equal(u, w)
+    assert np.array_equal(sa, sb)
+    for k in ("x", "y", "step", "path_len", "puzzle", "outcome", "visited"):
+        assert np.array_equal(np.asarray(xa[k]), np.asarray(xb[k])), k

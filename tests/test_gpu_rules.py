@@ -145,8 +145,6 @@ def test_rollout_rule_bits_every_step(on_gpu, sizes, max_shaped):
     pids = (np.arange(n) * 37) % len(proc)
     acts = torch.randint(0, 4, (T, n), dtype=torch.uint8, device="cuda")
     a = SPaRCVecEnv(n, **kw)
-    if generic:
-        a.core.set_variant(a.core.VARIANT_RULE_ROLLOUT_GENERIC, 1)
     a.reset(options={"puzzle_index": pids})
     ra = a.rollout(T, acts, rules=True)
     b = SPaRCVecEnv(n, **kw)

@@ -11,7 +11,7 @@ no size limits), and the exact-fit queue past its first capacity.
   instance per cell centre, 49 on a 15 x 15 lattice, so the GPU search's 64-poly list never
   overflows.)
 * The exact-fit queue (65,536 entries at first) overflowing: with the GPU's node cap at 1 every
-  search is queued; a generic rule rollout of 4,096 envs x 32 steps (131,072 audits) and a
+  search is queued; a generic rule rollout of 8,192 envs x 48 steps (393,216 audits) and a
   k_rules audit of 65,536 envs queue more than the queue holds, sparc_rules_finish grows it and
   runs the call again from the state it started from; bits, rewards, flags, stats and state equal
   the same calls with the default cap (no searches queued) and, on samples, the oracle.
@@ -69,6 +69,58 @@ def _add_instances(rec, rng, n_ylops, n_polys, shape_fn, up_to=False):
     return rec
 
 
+def _walled(rec, shape_fn, n_ylops, n_polys):
+    """A 15 x 15 record split by a wall of gap points at lattice column wx (SPaRC_Gym.py:423-454:
+    gaps block the region flood): region 0, the cells left of the wall, holds one vertical
+    7-cell bar poly per cell column (its exact fit succeeds); region 1 holds n_ylops / n_polys
+    more instances (shape_fn(k)) whose area check fails.  With 17 ylops or 17 distinct poly
+    shapes the puzzle is past the GPU search's lists, so region 0's search runs on the host."""
+    from sparc_gym_amd.puzzles import safe_load
+    from sparc_gym_amd.synthetic import _dump
+    text = safe_load(rec["text_visualization"])
+    sx, ex = text["puzzle"]["start"]["x"], text["puzzle"]["end"]["x"]
+    wx = next(x for x in (4, 6, 8, 10, 2, 12) if x not in (sx, ex))
+    cells = [c for c in text["puzzle"]["cells"] if (c["position"]["x"], c["position"]["y"]) != (wx, 0)]
+    for y in range(15):
+        cells.append({"position": {"x": wx, "y": y}, "properties": {"gap": True}})
+    poly, sid = {}, 700000
+    left = [(x, 1) for x in range(1, wx, 2)]
+    right = [(x, y) for x in range(wx + 1, 15, 2) for y in range(1, 15, 2)]
+    poly[str(sid)] = [[1] * 7]   # dx = array row, dy = array column (_get_offsets 840-855)
+    inst = [(c, "poly", sid) for c in left]
+    for k in range(n_ylops + n_polys):
+        poly[str(sid + 1 + k)] = shape_fn(k)
+        inst.append((right[k], "ylop" if k < n_ylops else "poly", sid + 1 + k))
+    for (x, y), kind, i in inst:
+        cells.insert(0, {"position": {"x": x, "y": y}, "properties": {"type": kind, "color": "red", "polyshape": i}})
+    text["puzzle"]["cells"] = cells
+    rec = dict(rec)
+    rec["text_visualization"] = _dump(text)
+    rec["polyshapes"] = _dump(poly)
+    return rec
+
+
+def _two_walls(rec):
+    """A 15 x 15 record with gap walls at lattice columns 2 and 12 and a vertical 7-cell bar poly
+    in each outer cell column (x = 1, 13), or None when the start is not between the walls: the
+    agent can never enter the outer regions, so every audit of this puzzle runs two exact-fit
+    searches (both fit)."""
+    from sparc_gym_amd.puzzles import safe_load
+    from sparc_gym_amd.synthetic import _dump
+    text = safe_load(rec["text_visualization"])
+    if not 4 <= text["puzzle"]["start"]["x"] <= 10:
+        return None
+    cells = [c for c in text["puzzle"]["cells"] if c["position"]["x"] not in (2, 12)]
+    cells += [{"position": {"x": x, "y": y}, "properties": {"gap": True}} for x in (2, 12) for y in range(15)]
+    cells = [{"position": {"x": x, "y": 1}, "properties": {"type": "poly", "color": "red", "polyshape": 700000}}
+             for x in (1, 13)] + cells
+    text["puzzle"]["cells"] = cells
+    rec = dict(rec)
+    rec["text_visualization"] = _dump(text)
+    rec["polyshapes"] = _dump({"700000": [[1] * 7]})
+    return rec
+
+
 def _limits_pool(n_base=1700):
     """n_base 15 x 15 puzzles (synthetic, base planes) with 40 polys each of random 5 x 5 shapes (more than 65,536 instances and 32,768 distinct shapes in all), then two puzzles past
     the GPU search's lists on an empty 15 x 15 base: 17 monomino ylops + 20 monomino polys (every
@@ -85,10 +137,10 @@ def _limits_pool(n_base=1700):
     recs = [_add_instances(r, rng, 0, 40, random_shape, up_to=True)
             for r in synthetic.make_puzzles(n_base, seed=31, sizes=((7, 7),), full_properties=False, n_solutions=1)]
     empty = synthetic.make_puzzles(2, seed=32, sizes=((7, 7),), full_properties=False)
-    recs.append(_add_instances(empty[0], rng, 17, 20, lambda _k: [[1]]))
     rects = [(4, 5), (5, 4), (4, 6), (6, 4), (5, 5), (4, 7), (7, 4), (5, 6), (6, 5), (5, 7), (7, 5), (6, 6),
              (6, 7), (7, 6), (7, 7), (3, 7), (7, 3)]
-    recs.append(_add_instances(empty[1], rng, 0, 17, lambda k: [[1] * rects[k][1]] * rects[k][0]))
+    recs.append(_walled(empty[0], lambda k: [[1]], 17, 0))
+    recs.append(_walled(empty[1], lambda k: [[1] * rects[k][1]] * rects[k][0], 0, 17))
     return recs
 
 
@@ -124,7 +176,11 @@ def test_rule_table_without_pool_limits_vs_oracle(on_gpu, limits_pool):
                       observation="compact", rules=True, max_steps=60)
     vec.reset(options={"puzzle_index": pids})
     refp = [dict(p) for p in proc]
-    seen_flagged_fit = 0
+    walled = [len(proc) - 2, len(proc) - 1]
+    assert counts[walled[0]][0] == 17 and counts[walled[1]][1] >= 17
+    pids[:64] = walled[0]
+    pids[64:128] = walled[1]
+    vec.reset(options={"puzzle_index": pids})
     for T in (0, 3, 9, 17):
         if T:
             vec.rollout(T, None, seed=T, record=False)
@@ -136,9 +192,10 @@ def test_rule_table_without_pool_limits_vs_oracle(on_gpu, limits_pool):
                                  rng.choice(n, 100, replace=False)])
         for i in sample:
             assert int(bits[i]) == _oracle_bits(refp, st, i, table.pitch), (T, i, int(st["puzzle"][i]))
-        fit = out["fit"].cpu().numpy()
-        seen_flagged_fit += int((fit[::2] != 0).sum())
-    assert seen_flagged_fit > 0   # the host ran searches of the flagged puzzles that succeeded
+        if T == 0:   # region 0 of the walled puzzles fits: searches the host ran (cap 0 on the GPU)
+            fit = out["fit"].cpu().numpy()
+            assert ((fit[:128] & 1) == 1).all()
+            assert vec.core.rules_queue_stats()["last_searches"] >= 128
 
 
 def test_sparc_gym_constructs_on_the_limits_pool(on_gpu, limits_pool):
@@ -151,7 +208,8 @@ def test_sparc_gym_constructs_on_the_limits_pool(on_gpu, limits_pool):
     rng = np.random.default_rng(9)
     checked = 0
     for q in (len(recs) - 2, len(recs) - 1):   # the 17-ylop puzzle, the 17-distinct-shape puzzle
-        env.reset(options={"puzzle_index": q})
+        env.reset(options={"puzzle_id": recs[q]["id"]})                               # SPaRC_Gym.py:1073-1079
+        assert env.current_puzzle_index == q
         p = dict(env.puzzles[q])
         for _ in range(12):
             _, _, term, trunc, info = env.step(int(rng.integers(4)))
@@ -168,18 +226,20 @@ def test_sparc_gym_constructs_on_the_limits_pool(on_gpu, limits_pool):
 
 @pytest.mark.parametrize("generic", [True, False])
 def test_exact_fit_queue_overflow_rerun(on_gpu, generic):
-    """fit_cap = 1: every exact-fit search is queued.  A rule rollout of 4,096 envs x 32 steps
-    (131,072 audits) on a pool without region-code tables (the generic rule kernel: 13x13 / 15x15
-    lattices) queues more searches than the first queue holds; so does one k_rules audit of
-    65,536 envs.  Their outputs equal the default cap's (nothing queued)."""
+    """fit_cap = 1: every exact-fit search is queued.  On a pool of two-walled puzzles
+    (_two_walls: two searches per audit, none on the GPU; 15 x 15 lattices have no region-code
+    table, so rule rollouts take the generic rule kernel) a rule rollout of 8,192 envs x 48 steps
+    (393,216 audits) queues far more searches than the first queue holds, and so does one k_rules
+    audit of 65,536 envs.  Their outputs equal the default cap's (every search on the GPU)."""
     from sparc_gym_amd import SPaRCVecEnv, synthetic
     from sparc_gym_amd.puzzles import process_puzzles
-    recs = synthetic.make_rule_puzzles(128, seed=41, sizes=((7, 7), (6, 6)), break_prob=0.3)
-    recs += synthetic.make_puzzles(128, seed=42, sizes=((7, 7), (6, 6)), full_properties=True, max_shaped=4)
+    recs = [r for r in map(_two_walls, synthetic.make_puzzles(200, seed=41, sizes=((7, 7),), full_properties=False,
+                                                                n_solutions=1)) if r is not None]
+    assert len(recs) > 50
     proc = process_puzzles(recs)
     refp = [dict(p) for p in proc]
     if generic:
-        n, T = 4096, 32
+        n, T = 8192, 48
         pids = np.arange(n) % len(proc)
         acts = torch.randint(0, 4, (T, n), dtype=torch.uint8, device="cuda")
         runs = []

@@ -29,9 +29,9 @@ from sparc_gym_amd.puzzles import pack_rules, pack_table, process_puzzles  # noq
 ap = argparse.ArgumentParser()
 ap.add_argument("--puzzles", type=int, default=100000)
 ap.add_argument("--distinct", type=int, default=1000)
-ap.add_argument("--full", type=int, default=20000,
-                help="puzzles with the full property set (the rest: base planes); the rule table's "
-                     "instance index is 16 bits, so all puzzles together hold < 65,536 poly/ylop instances")
+ap.add_argument("--full", type=int, default=100000,
+                help="puzzles with the full property set (the rest: base planes); the rule table has no "
+                     "pool-wide limit (32-bit instance offsets, 21-bit shape ids)")
 ap.add_argument("--grid", type=int, nargs=2, default=(3, 4))
 a = ap.parse_args()
 t0 = time.perf_counter()
