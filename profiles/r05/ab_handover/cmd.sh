@@ -1,0 +1,12 @@
+source tools/gpu_run.sh
+for r in 1 2 3; do
+  for v in head_HEAD new la lamask; do
+    if [ $v = new ]; then L=""; else L="--lib ab/lib_$v.so"; fi
+    step c3_${v}_$r 240 python tools/prof_rollout.py --config c3 --chunk 2000 --launches 20 --time $L
+  done
+  for v in head_HEAD new lamask2; do
+    if [ $v = new ]; then L=""; else L="--lib ab/lib_$v.so"; fi
+    step c2_${v}_$r 240 python tools/prof_rollout.py --config c2 --envs 4096 --chunk 2000 --launches 20 --time $L
+  done
+done
+step gputests 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider

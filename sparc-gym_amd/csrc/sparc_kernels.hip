@@ -237,6 +237,78 @@ __device__ __forceinline__ void obs_write(const ObsWave<W>* ow, const uint16_t* 
     }
 }
 
+// Bit-stream staging (k_rollout_obsw on multi-word pools, whose board bit x * pitch + y IS plane
+// cell x * YD + y: pitch == YD).  The planes of a wave's 64 envs are one run of 64 * XY entries,
+// entry f = env l, cell f - l * XY; staged as two bit streams (visited, agent) in which bit f is
+// entry f, every piece of 4 entries is 4 bits of one 32-bit word, whichever env they belong to:
+// the writer reads one word per plane and piece (against 12 LDS reads and ~30 VALU through the
+// LUT) and zeroes the words it has read for the next use of the buffer.  Each compute lane ORs its
+// board, shifted to bit l * XY, into the stream (ds_or_b32: the end words are shared with the
+// neighbour envs).
+template <int W>
+struct ObsStream {
+    uint32_t vis[128 * W + 1];   // 64 envs x at most 64 W bits, + the last lane's shifted spill
+    uint32_t ag[128 * W + 1];
+};
+// stream staging applies: the board bit of cell (x, y) is x * YD + y
+template <int W>
+__host__ __device__ constexpr bool obs_stream_ok(uint32_t pitch, uint32_t YD) { return W > 1 && pitch == YD; }
+
+template <int W>
+__device__ __forceinline__ void obs_stage_stream(ObsStream<W>* os, uint32_t lane, bool has_env,
+                                                 const uint64_t (&v)[W], uint32_t ab, uint32_t XY) {
+    if (!has_env) return;
+    const uint32_t o = lane * XY, w0 = o >> 5, sh = o & 31u;
+    uint32_t b[2 * W];
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+        b[2 * k] = (uint32_t)v[k];
+        b[2 * k + 1] = (uint32_t)(v[k] >> 32);
+    }
+    // word j of the board shifted up by sh (bits at and above XY are 0: the board has none)
+#pragma unroll
+    for (int j = 0; j <= 2 * W; ++j) {
+        const uint64_t pair = ((uint64_t)(j < 2 * W ? b[j] : 0u) << 32) | (j > 0 ? b[j - 1] : 0u);
+        atomicOr(&os->vis[w0 + j], (uint32_t)(pair >> (32u - sh)));
+    }
+    const uint32_t a = o + ab;
+    atomicOr(&os->ag[a >> 5], 1u << (a & 31u));
+}
+
+// the staged envs [0, cnt) -> planes at vout / aout (run starts); zeroes the words it read.
+// Every lane of the writing wave calls this (wave-uniform)
+template <int W>
+__device__ __forceinline__ void obs_write_stream(ObsStream<W>* os, uint32_t lane, uint32_t cnt, uint32_t XY,
+                                                 int32_t* __restrict__ vout, int32_t* __restrict__ aout) {
+    const uint32_t total = cnt * XY;
+    const bool vec = (((reinterpret_cast<uintptr_t>(vout) | reinterpret_cast<uintptr_t>(aout)) & 15u) == 0);
+    for (uint32_t f = 4u * lane; f < total; f += 256u) {
+        const uint32_t wv = os->vis[f >> 5], wa = os->ag[f >> 5], sh = f & 31u;
+        uint32_t vv[4], aa[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            vv[k] = __builtin_amdgcn_ubfe(wv, sh + k, 1u);
+            aa[k] = __builtin_amdgcn_ubfe(wa, sh + k, 1u);
+        }
+        if (sh == 0u) {   // after the reads of all 8 lanes of this word (in order within the wave)
+            os->vis[f >> 5] = 0u;
+            os->ag[f >> 5] = 0u;
+        }
+        if (vec && f + 4u <= total) {
+            if (vout) __builtin_nontemporal_store(u32x4{vv[0], vv[1], vv[2], vv[3]}, reinterpret_cast<u32x4*>(vout + f));
+            if (aout) __builtin_nontemporal_store(u32x4{aa[0], aa[1], aa[2], aa[3]}, reinterpret_cast<u32x4*>(aout + f));
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (f + k < total) {
+                    if (vout) vout[f + k] = (int32_t)vv[k];
+                    if (aout) aout[f + k] = (int32_t)aa[k];
+                }
+            }
+        }
+    }
+}
+
 // step() + the 'new' observation in one launch (SPaRCVecEnv.step): the gym one-call-per-step
 // contract with the planes, the puzzle index and the agent (x | y << 8) of every env
 // the gym outputs of sparc_step_gym_device (each pointer may be null) and the action width
@@ -564,40 +636,55 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Params p, int32_t T, const u
 // so a wave that both gathers trie records and stores planes (k_rollout<..., OBS>) waits, at each
 // step's record wait, for every plane store it issued in the step before: its stores drain in
 // bursts (MI355X, c4: 62-78 % of 8 TB/s, 0.71 of the box's fill_ bandwidth).  Here a workgroup of
-// 256 envs has 4 compute waves (Env<W>, one lane per env) and one writer wave: in iteration t the
+// 256 envs has 4 compute waves (Env<W>, one lane per env) and 4 writer waves: in iteration t the
 // compute waves run step t and stage each env's board and agent bit in LDS buffer t % 2
-// (obs_stage), while the writer streams the planes of step t - 1 from the other buffer
-// (obs_write: 16-B pieces of each 64-env run, every store instruction 1 KB of contiguous memory);
-// one barrier per step hands the buffers over.  The writer issues no load and never waits for its
-// stores; the compute waves' own stores are a byte of reward code and of flags per env-step.
-constexpr int kBlockOw = 320;
+// (obs_stage), while writer k streams the planes of step t - 1 of compute wave k's envs from the
+// other buffer (obs_write: 16-B pieces of each 64-env run, every store instruction 1 KB of
+// contiguous memory); one barrier per step hands the buffers over.  The writers issue no load and
+// never wait for their stores; the compute waves' own stores are a byte of reward code and of
+// flags per env-step.  One writer per workgroup was issue-bound (the plane assembly is ~40
+// instructions and 12 LDS reads per 16-B piece: MI355X, c4 3.26 ms per launch against 2.54 ms
+// inline)
+constexpr int kBlockOw = 512;
+// one staging buffer: ObsWave (LUT path) or ObsStream (bit streams), [2 steps][4 compute waves]
+template <int W>
+__host__ __device__ constexpr size_t obsw_buf_bytes() {
+    return ((sizeof(ObsWave<W>) > sizeof(ObsStream<W>) ? sizeof(ObsWave<W>) : sizeof(ObsStream<W>)) + 15) / 16 * 16;
+}
 template <int W, bool TB>
 __host__ __device__ constexpr size_t obsw_lds_bytes() {
-    return 8 * sizeof(ObsWave<W>) + kObsCells * sizeof(uint16_t) + ((W == 1 && TB) ? 4 * 64 * 64 : 0);
+    return 8 * obsw_buf_bytes<W>() + kObsCells * sizeof(uint16_t) + ((W == 1 && TB) ? 4 * 64 * 64 : 0);
 }
 template <int W, bool TB, bool RAND>
-__global__ void __launch_bounds__(kBlockOw) __attribute__((amdgpu_waves_per_eu(5)))
+__global__ void __launch_bounds__(kBlockOw) __attribute__((amdgpu_waves_per_eu(4)))
     k_rollout_obsw(Params p, int32_t T, const uint8_t* __restrict__ act, uint64_t seed, uint64_t t0,
                    int8_t* __restrict__ rew, uint8_t* __restrict__ flg, int4* __restrict__ stats, ObsTrace ot) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    ObsWave<W>* ob = reinterpret_cast<ObsWave<W>*>(smem);   // [2 buffers][4 compute waves]
-    uint16_t* lut = reinterpret_cast<uint16_t*>(smem + 8 * sizeof(ObsWave<W>));
-    obs_build_lut(lut, ot.XD, ot.YD, p.pitch, W, threadIdx.x, kBlockOw);
+    constexpr size_t kBuf = obsw_buf_bytes<W>();   // buffer (t & 1) * 4 + k at smem + that * kBuf
+    uint16_t* lut = reinterpret_cast<uint16_t*>(smem + 8 * kBuf);
+    const bool stream = obs_stream_ok<W>(p.pitch, ot.YD);   // block-uniform
+    if (stream) {   // the bit streams start at 0 (the writers zero them after each read)
+        for (uint32_t k = threadIdx.x; k < 8 * kBuf / 4; k += kBlockOw) reinterpret_cast<uint32_t*>(smem)[k] = 0u;
+    } else {
+        obs_build_lut(lut, ot.XD, ot.YD, p.pitch, W, threadIdx.x, kBlockOw);
+    }
     __syncthreads();
+    auto buf = [&](uint32_t j) { return smem + j * kBuf; };
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const size_t n = p.n;
     const uint32_t XY = ot.XD * ot.YD;
-    if (wv == 4) {                                               // ---- the writer wave
+    if (wv >= 4) {                                               // ---- the writer waves
+        const uint32_t k = wv - 4u;                              // compute wave k's envs
+        const size_t wb = (size_t)blockIdx.x * 256u + k * 64u;
+        const uint32_t cnt = wb >= n ? 0u : (n - wb < 64u ? (uint32_t)(n - wb) : 64u);
         for (int32_t t = 0; t <= T; ++t) {
-            if (t > 0) {
-                for (uint32_t k = 0; k < 4; ++k) {
-                    const size_t wb = (size_t)blockIdx.x * 256u + k * 64u;
-                    if (wb >= n) break;
-                    const uint32_t cnt = n - wb < 64u ? (uint32_t)(n - wb) : 64u;
-                    const size_t run = ((size_t)(t - 1) * n + wb) * XY;
-                    obs_write<W>(ob + ((t - 1) & 1) * 4 + k, lut, lane, cnt, XY, ot.vout ? ot.vout + run : nullptr,
-                                 ot.aout ? ot.aout + run : nullptr);
-                }
+            if (t > 0 && cnt > 0) {
+                const size_t run = ((size_t)(t - 1) * n + wb) * XY;
+                uint8_t* bk = buf(((t - 1) & 1) * 4 + k);
+                int32_t* vo = ot.vout ? ot.vout + run : nullptr;
+                int32_t* ao = ot.aout ? ot.aout + run : nullptr;
+                if (stream) obs_write_stream<W>(reinterpret_cast<ObsStream<W>*>(bk), lane, cnt, XY, vo, ao);
+                else obs_write<W>(reinterpret_cast<const ObsWave<W>*>(bk), lut, lane, cnt, XY, vo, ao);
             }
             __syncthreads();                                     // B_t
         }
@@ -608,7 +695,7 @@ __global__ void __launch_bounds__(kBlockOw) __attribute__((amdgpu_waves_per_eu(5
     const PuzzleSrc<W> src{p.tab.info, p.tab.root, p.tab.open, p.tab.init, p.tab.row1};
     using Stack = typename std::conditional<(W == 1 && TB), LdsStack<64>, RegStack>::type;
     Env<W, TB, Stack> e;
-    if constexpr (W == 1 && TB) e.stk.col = smem + 8 * sizeof(ObsWave<W>) + kObsCells * sizeof(uint16_t) + wv * 64 * 64 + lane;
+    if constexpr (W == 1 && TB) e.stk.col = smem + 8 * kBuf + kObsCells * sizeof(uint16_t) + wv * 64 * 64 + lane;
     if (active) e.load(p, src, i);
     int4 acc = make_int4(0, 0, 0, 0);
     const uint64_t gid = p.env_offset + i;
@@ -629,7 +716,9 @@ __global__ void __launch_bounds__(kBlockOw) __attribute__((amdgpu_waves_per_eu(5
             acc.w += (f & 64u) ? 1 : 0;
             e.obs_words(p, src, v, ab);
         }
-        obs_stage<W>(ob + (t & 1) * 4 + wv, lane, active, v, ab);
+        uint8_t* bk = buf((t & 1) * 4 + wv);
+        if (stream) obs_stage_stream<W>(reinterpret_cast<ObsStream<W>*>(bk), lane, active, v, ab, XY);
+        else obs_stage<W>(reinterpret_cast<ObsWave<W>*>(bk), lane, active, v, ab);
         __syncthreads();                                         // B_t
     }
     __syncthreads();                                             // B_T: the writer's last step
@@ -821,7 +910,7 @@ __global__ void __launch_bounds__(kBlock1) k_rollout1(Params p, int32_t T, const
 // gathers, the reward code and the episode counters one 16-step tile behind.  Nothing flows
 // back: the reward code never feeds the move.  I/O waves stream action tiles in (the actions
 // for the trie wave, each action's target window position for the move wave) and reward / flag
-// tiles out (the flag byte is byte 2 of the hand-over word).  Per workgroup 256 envs = 4 move waves (0-3) + 4 trie waves (4-7, on
+// tiles out (the flag bytes from the hand-over words, flag_bytes4).  Per workgroup 256 envs = 4 move waves (0-3) + 4 trie waves (4-7, on
 // the same SIMDs as the move waves of their envs) + 4 I/O waves (8-11, one per SIMD); one
 // barrier per tile:
 //   interval k (between barriers B_k and B_k+1): move waves step tile k; trie waves finish
@@ -858,11 +947,29 @@ __device__ __forceinline__ uint32_t clamp_actions4(uint32_t x) {
     return (x & ~bm) | (bm & 0x04040404u);
 }
 
-// the flag bytes (byte 2, sparc_move1.hpp) of four hand-over words
-__device__ __forceinline__ uint32_t flag_bytes4(const u32x4 w) {
-    const uint32_t lo = __builtin_amdgcn_perm(w.y, w.x, 0x0C0C0602u);
-    const uint32_t hi = __builtin_amdgcn_perm(w.w, w.z, 0x0C0C0602u);
-    return lo | (hi << 16);
+// byte b of four words, side by side (sel = 0x0C0C0400 + b * 0x0101)
+__device__ __forceinline__ uint32_t bytes4(const u32x4 w, uint32_t sel) {
+    return __builtin_amdgcn_perm(w.y, w.x, sel) | (__builtin_amdgcn_perm(w.w, w.z, sel) << 16);
+}
+// the flag bytes (term | trunc << 1 | legal << 2 | autoreset << 6) of four hand-over words of
+// the W = 1 move wave (sparc_move1.hpp), four bytes side by side; magic = legal_magic(pitch).
+// The legal bits: lw * magic carries the window bits right / up / left / down to bits 18..21
+// (v_mul_u32_u24 reads bits 0..23 of the word: lw alone).  Byte 3 holds at-target (bit 0) and
+// done (bit 1); at-target without done marks an autoreset step
+__device__ __forceinline__ uint32_t flag_bytes4(const u32x4 w, uint32_t magic) {
+    u32x4 m;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        uint32_t t;
+        asm("v_mul_u32_u24 %0, %1, %2" : "=v"(t) : "v"(w[j]), "s"(magic));
+        m[j] = t;
+    }
+    const uint32_t L = bytes4(m, 0x0C0C0602u) & 0x3C3C3C3Cu;          // legal << 2
+    const uint32_t B = bytes4(w, 0x0C0C0703u);                         // tgt | done << 1
+    const uint32_t term = B & (B >> 1) & 0x01010101u;                  // done at the target
+    const uint32_t trunc = B & ~(B << 1) & 0x02020202u;                // done elsewhere
+    const uint32_t rs = (B << 6) & ~(B << 5) & 0x40404040u;            // at-target, not done
+    return term | trunc | L | rs;
 }
 
 // k_rollout1s<…, IOR> (next-step autoreset): the reward codes of four env-steps from their
@@ -990,19 +1097,19 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const u32x4 hw = fh[j];
-                    f[j] = flag_bytes4(hw);
+                    f[j] = flag_bytes4(hw, p.lmagic);
                     v[j] = io_codes4(hw, f[j], tb[j], ct.cy[j], ct.cz[j], ct.cp[j], ct.cm[j]);
                 }
                 if (rew) nt_store16(reinterpret_cast<uint8_t*>(rew) + o, v);
                 if (flg) nt_store16(flg + o, f);
             } else {
                 if (rew) nt_store16(reinterpret_cast<uint8_t*>(rew) + o, *reinterpret_cast<const u32x4*>(base + kS_Rew));
-                if (flg) {   // byte 0 of 16 hand-over words
+                if (flg) {   // the flag bytes of 16 hand-over words
                     u32x4 v;
-                    v.x = flag_bytes4(fh[0]);
-                    v.y = flag_bytes4(fh[1]);
-                    v.z = flag_bytes4(fh[2]);
-                    v.w = flag_bytes4(fh[3]);
+                    v.x = flag_bytes4(fh[0], p.lmagic);
+                    v.y = flag_bytes4(fh[1], p.lmagic);
+                    v.z = flag_bytes4(fh[2], p.lmagic);
+                    v.w = flag_bytes4(fh[3], p.lmagic);
                     nt_store16(flg + o, v);
                 }
             }
@@ -1048,6 +1155,7 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         if constexpr (LDS_TABLE) m.prefetch_reset(mrow, pid0 + 1 == NP ? 0u : pid0 + 1);
         else m.prefetch_reset_g(mrow, trow, pid0 + 1 == NP ? 0u : pid0 + 1);
         const uint32_t pend0 = m.pending ? 1u : 0u;
+        const bool ar = IOR || p.autoreset == 1;   // IOR kernels serve next-step autoreset only
         const uint64_t gid = p.env_offset + i;
         uint32_t* th = reinterpret_cast<uint32_t*>(pb + kS_FH) + lane;
         __syncthreads();                                         // B_0
@@ -1072,9 +1180,10 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const uint32_t row = (uint32_t)(k * kTile + g + j) & (kRing - 1);
-                    if constexpr (LDS_TABLE) m.reset_next(p, mrow, col_addr);
-                    else m.reset_next_g(p, mrow, trow, col_addr, slot_addr);
-                    th[row * 64] = m.step_pos(p, pv[j]);
+                    bool rs;
+                    if constexpr (LDS_TABLE) rs = m.reset_next(ar, mrow, col_addr);
+                    else rs = m.reset_next_g(ar, mrow, trow, col_addr, slot_addr);
+                    th[row * 64] = m.step_pos(p, pv[j], rs);
                 }
             }
             if constexpr (!LDS_TABLE) m.tile_end();
@@ -1153,7 +1262,7 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
             __syncthreads();                                     // B_{k+1}
         }
         if constexpr (IOR)   // the last step's hand-over word is still in the ring
-            if (K > 0) tl.finish_oneg(th[((uint32_t)(K * kTile - 1) & (kRing - 1)) * 64u] & 0x30000u);
+            if (K > 0) tl.finish_oneg(th[((uint32_t)(K * kTile - 1) & (kRing - 1)) * 64u] & kHwDone);
         if constexpr (IOR) {
             fin[0] = make_uint4(tl.S, (uint32_t)tl.Oneg, tl.pid, 0u);
         } else {

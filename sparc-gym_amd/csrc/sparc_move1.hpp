@@ -16,18 +16,22 @@
 //    (bias: len >= 3, or len == 2 with an open start);
 //  * the stack holds the back positions (2P - pos of each move), so the pop needs no
 //    direction arithmetic;
-//  * the legal-action mask (1024-1051) is not built in action order: its window bits
-//    lw = (w & NBM) | bias << rp are multiplied by one constant (p.lmagic) that carries the
-//    four bits right / up / left / down to bits 18..21 without carries (every partial product
-//    lands on its own bit), so the flag byte (term | trunc << 1 | legal << 2 | reset << 6)
-//    is byte 2 of the hand-over word and the I/O wave stores it with one byte select;
-//  * lw == 0 is the empty legal set (truncation, 1195).
+//  * the legal-action mask (1024-1051) and the flag byte are not built here: the word carries
+//    the step's legal window bits lw = (w & NBM) | bias << rp, at-target and done, and the I/O
+//    wave turns four words into four flag bytes (flag_bytes4, sparc_kernels.hip: the legal bits
+//    via one multiply by p.lmagic, which carries the four bits right / up / left / down to bits
+//    18..21 without carries);
+//  * lw == 0 is the empty legal set (truncation, 1195);
+//  * an autoreset step hands over at-target set and done clear, a pair no other step has (at the
+//    target is done), so the reset needs no bit of its own.
 //
 // Hand-over word (to the trie wave and the I/O wave):
-//   bits 16..23  the flag byte (bit 16 terminated, 17 truncated, 18..21 legal, 22 autoreset)
+//   bits 0..18   lw (window bits of the legal actions after the step)
+//   bit 24       at the target, or an autoreset step
+//   bit 25       done: terminated or truncated (0 on an autoreset step)
 //   bits 30..31  fwd - pop, two's complement (+1 forward, -1 pop, 0 no move)
 //   other bits   0
-// Valid for pitches 3..9 (host-checked): the constant needs 2P <= 18.
+// Valid for pitches 3..9 (host-checked): the legal-bit constant needs 2P <= 18.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -36,7 +40,9 @@
 
 namespace sparc {
 
-constexpr uint32_t kHwTerm = 0x10000u, kHwTrunc = 0x20000u, kHwReset = 0x400000u, kHwLegal = 0x3C0000u;
+constexpr uint32_t kHwLw = 0x7FFFFu, kHwTgt = 1u << 24, kHwDone = 1u << 25;
+// the step of hand-over word hw was an autoreset step
+__device__ __forceinline__ bool hw_reset(uint32_t hw) { return (hw & (kHwTgt | kHwDone)) == kHwTgt; }
 
 // Row slots (k_rollout1s on pools past the LDS row budget).  The trie wave runs one tile behind
 // the move wave, so the move wave, which reads both rows of the next puzzle from the L2 at the
@@ -74,11 +80,11 @@ template <bool TB>
 struct MoveLane1 {
     uint64_t fr = 0;          // free board, one row up (bit e + P = point e)
     uint32_t e = 0, w = 0;    // agent bit; window (fr >> e) between steps, 0 on a reset step
-    uint32_t tgt = 0, pflags = 0, pending = 0, len = 1;
+    uint32_t tgt = 0, pflags = 0, len = 1;
+    bool pending = false;                 // the last step was done (not an autoreset step)
     int32_t step = 0;
     uint32_t sp = 0, bks = 0, bias = 0;   // traceback: stack slot len-1 (LDS byte address), rule bias
     uint32_t rp = 0, pnr = 0;             // traceback: back position of the last move / the one before
-    uint32_t lv = 0x30000u;               // flag-bit mask of the step: term | trunc, or kHwReset
     uint4 rr = {0u, 0u, 0u, 0u};          // the next autoreset's move row: row word, free board, the puzzle after it
     // global rows (k_rollout1s<…, LDS_TABLE = false>, row_slots below): the next autoreset's trie
     // row, handed to the trie wave through its slot; this launch's reset count and the tile
@@ -105,13 +111,15 @@ struct MoveLane1 {
 
     // gymnasium next-step autoreset (reset(), SPaRC_Gym.py:1087): the next puzzle's row and
     // board from registers (read at the previous reset); the step then moves nowhere (w = 0,
-    // bias = 0) and reports the reset flag instead of term / trunc (lv).  The row of the reset
+    // bias = 0), is never done and hands over at-target (step_pos); returns whether it reset.  ar:
+    // p.autoreset == 1 (a compile-time true in the kernels that serve only that mode).  The row of the reset
     // after it is read inside the branch straight into the same registers, so nothing waits for
     // it until the next reset (at least two steps later: a reset step is never done).  Copied
     // on from temporaries instead, the branch waited for the LDS read on every reset (about a
     // fifth of all wave-steps take the branch)
-    __device__ __forceinline__ void reset_next(const Params& p, const uint4* mrow, uint32_t col_addr) {
-        if ((pending != 0u) & (p.autoreset == 1)) {
+    __device__ __forceinline__ bool reset_next(const bool ar, const uint4* mrow, uint32_t col_addr) {
+        const bool rs = pending & ar;
+        if (rs) {
             e = rr.x & 0xFFu;
             tgt = (rr.x >> 8) & 0xFFu;
             pflags = rr.x >> 16;
@@ -125,12 +133,12 @@ struct MoveLane1 {
                 len = 1;
             }
             step = -1;   // this step's increment brings it to 0
-            lv = kHwReset;
             // keep the uses of the old row above the read (as TrieLane::step_core): without this
             // the compiler issued the read first into temporaries and waited for it in the branch
             __asm__ volatile("" ::"v"(fr), "v"(e), "v"(tgt), "v"(pflags) : "memory");
             rr = mrow[rr.w];
         }
+        return rs;
     }
 
     // the same from global rows: the move row and the trie row of the next puzzle are read from
@@ -142,9 +150,10 @@ struct MoveLane1 {
         rg = ld_off(reinterpret_cast<const v4u*>(mrow), q << 4);
         rt = ld_off(reinterpret_cast<const v4u*>(trow), q << 4);
     }
-    __device__ __forceinline__ void reset_next_g(const Params& p, const uint4* __restrict__ mrow,
+    __device__ __forceinline__ bool reset_next_g(const bool ar, const uint4* __restrict__ mrow,
                                                  const uint4* __restrict__ trow, uint32_t col_addr, uint32_t slot_addr) {
-        if ((pending != 0u) & (p.autoreset == 1)) {
+        const bool rs = pending & ar;
+        if (rs) {
             e = rg.x & 0xFFu;
             tgt = (rg.x >> 8) & 0xFFu;
             pflags = rg.x >> 16;
@@ -158,7 +167,6 @@ struct MoveLane1 {
                 len = 1;
             }
             step = -1;
-            lv = kHwReset;
             const uint32_t s = nres < lim ? (nres & (kRowSlots - 1u)) : kRowSlots;
             *(lds_v4*)(uintptr_t)(slot_addr + s * kRowSlotStride) = rt;
             nres += 1u;
@@ -167,6 +175,7 @@ struct MoveLane1 {
             rg = ld_off(reinterpret_cast<const v4u*>(mrow), q);
             rt = ld_off(reinterpret_cast<const v4u*>(trow), q);
         }
+        return rs;
     }
     // after each tile: lim = resets through the tile before last + kRowSlots (row_slots)
     __device__ __forceinline__ void tile_end() {
@@ -174,9 +183,9 @@ struct MoveLane1 {
         cA = nres;
     }
 
-    // one env-step's move part (1131-1199) from the target's window position; returns the
-    // hand-over word
-    __device__ __forceinline__ uint32_t step_pos(const Params& p, uint32_t pos) {
+    // one env-step's move part (1131-1199) from the target's window position; rs: the step is an
+    // autoreset step (reset_next).  Returns the hand-over word
+    __device__ __forceinline__ uint32_t step_pos(const Params& p, uint32_t pos, bool rs) {
         const uint32_t P = p.pitch;
         step = __builtin_elementwise_add_sat(step, 1);                              // 1132
         const bool trunc0 = step >= p.max_steps;                                    // 1134
@@ -207,17 +216,11 @@ struct MoveLane1 {
         if constexpr (TB) lw |= bias << rp;
         const bool at_tgt = e == tgt;                                                // 1192
         const bool done = trunc0 | (lw == 0u) | at_tgt;                             // 1195-1199
-        // term | trunc << 1 at bits 16-17 (trunc = done and not term), or the reset bit
-        const uint32_t fb = (((done ? kHwTrunc : 0u) - (at_tgt ? kHwTerm : 0u)) | kHwReset) & lv;
-        pending = fb & (kHwTerm | kHwTrunc);
+        // an autoreset step is never done (w = 0 before it: lw was 0) and reports at-target
+        pending = done & !rs;
         // the move before the last (slot len-3 after the step), for the next pop
         if constexpr (TB) pnr = *lds_byte(sp - 128u);
-        lv = kHwTerm | kHwTrunc;
-        // lw * lmagic < 2^48 and only bits 18-21 are kept: v_mul_u32_u24, written out (the
-        // compiler selects the quarter-rate v_mul_lo_u32 for __umul24 here)
-        uint32_t prod;
-        asm("v_mul_u32_u24 %0, %1, %2" : "=v"(prod) : "v"(lw), "s"(p.lmagic));
-        return (prod & kHwLegal) | fb | ((uint32_t)dl << 30);
+        return ((uint32_t)dl << 30) | ((at_tgt | rs) ? kHwTgt : 0u) | (pending ? kHwDone : 0u) | lw;
     }
 
     // ---- SoA <-> registers / LDS stack (launch start and end; the Env<1> state format)
@@ -229,14 +232,13 @@ struct MoveLane1 {
         const uint32_t pid = s.pid[i];
         e = (ps & 0xFFu) * P + ((ps >> 8) & 0xFFu);
         len = (ps >> 16) & 0xFFu;
-        pending = (ax >> 18) & 1u;
+        pending = ((ax >> 18) & 1u) != 0u;
         step = (int32_t)s.step[i];
         const uint4 r = p.tab.row1[pid];
         tgt = (r.x >> 8) & 0xFFu;
         pflags = r.x >> 16;
         fr = (p.tab.open[pid] & ~vis) << P;
         w = (uint32_t)(fr >> (e & 63u));
-        lv = kHwTerm | kHwTrunc;
         if constexpr (TB) {
             const uint32_t moves = len >= 1 ? len - 1 : 0u;
             const uint64_t lo = s.dirs[i], hi = s.dirs[(size_t)p.n + i];

@@ -4,11 +4,12 @@
 // np.array_equal test of 1206) walks a per-puzzle trie of the solution paths.  It needs from
 // the move wave only what the move did, so in the split kernels a TRIE wave runs it one tile
 // behind the move wave of the same 64 envs, from a hand-over word per env-step and the step's
-// action (which the trie wave reads from the action tile itself).  The word carries the flag
-// byte (term | trunc << 1 | legal << 2 | autoreset << 6) and fwd - pop (+1 forward move, -1
-// traceback pop, 0 no move); step() decodes the multi-word kernel's layout (widen_hand_word,
-// sparc_movew.hpp: flag byte at bits 0-7, fwd - pop at 16-31), step1() the W = 1 move wave's
-// (sparc_move1.hpp: flag byte at bits 16-23, fwd - pop at 30-31).
+// action (which the trie wave reads from the action tile itself).  The word tells whether the
+// step was an autoreset step and done, and fwd - pop (+1 forward move, -1 traceback pop, 0 no
+// move); step() decodes the multi-word kernel's layout (widen_hand_word, sparc_movew.hpp: flag
+// byte term | trunc << 1 | legal << 2 | autoreset << 6 at bits 0-7, fwd - pop at 16-31), step1()
+// the W = 1 move wave's (sparc_move1.hpp: autoreset iff bit 24 set and bit 25 clear, done at
+// bit 25, fwd - pop at 30-31).
 //
 // Geometry-independent: the same lane serves the W = 1 and the multi-word kernels.
 //
@@ -29,6 +30,7 @@
 #include <stdint.h>
 
 #include "sparc_env.hpp"
+#include "sparc_move1.hpp"
 
 namespace sparc {
 
@@ -37,6 +39,13 @@ namespace sparc {
 // itself a solution) when some solution starts at start, else 0x10000 (off the trie from the
 // start).  Rootless: children 0xFFFF.
 struct TrieLane {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) v4u lds_v4;
+    // row q of a row table (LDS or global) as one 4-vector, so that a read lands in one register tuple
+    template <class Rows>
+    __device__ __forceinline__ static v4u row4(const Rows& t, uint32_t q) {
+        return *reinterpret_cast<const v4u*>(&t[q]);
+    }
     uint32_t S = 0;
     int32_t Oneg = -100;
     uint32_t rx = ~0u, ry = ~0u;   // record of the current node (S & 0x7FFF)
@@ -44,7 +53,7 @@ struct TrieLane {
     int32_t hs = 0, hsn = 0;        // the puzzle has solutions (the +-1 rewards apply, 1217); -hs
     uint32_t hsb = 0;               // hs << 2 (the class byte's bit 2, CODES = false)
     uint32_t pid = 0, npid = 0;
-    uint4 nx;                       // trie row of npid, read at the previous reset
+    v4u nx;                         // trie row of npid, read at the previous reset
     int acc_x = 0;                  // sum of reward codes
     uint32_t acc_y = 0, acc_z = 0;  // done steps, done steps on a solution
 
@@ -73,7 +82,7 @@ struct TrieLane {
             ry = rec.y;
         }
         npid = next_pid(q, num_puzzles);
-        nx = trow[npid];
+        nx = row4(trow, npid);
     }
 
     // ---- row slots (k_rollout1s on pools past the LDS row budget; sparc_move1.hpp row_slots):
@@ -82,8 +91,6 @@ struct TrieLane {
     // from the L2 when the slot rule failed for that reset
     uint32_t nres = 0, lim = 0, cA = 0, slot_addr = 0;
     uint4 nxs = {0u, 0u, 0u, 0u};
-    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-    typedef __attribute__((address_space(3))) v4u lds_v4;
     __device__ __forceinline__ void slot_read(uint32_t slots, uint32_t stride) {
         const v4u v = *(const lds_v4*)(uintptr_t)(slot_addr + (nres & (slots - 1u)) * stride);
         nxs = make_uint4(v.x, v.y, v.z, v.w);
@@ -96,9 +103,9 @@ struct TrieLane {
     template <bool CODES, uint32_t SLOTS, uint32_t STRIDE, class Rows>
     __device__ __forceinline__ int step1s(const uint32_t hw, const uint32_t a, const Rows& trow,
                                           const uint2* __restrict__ trie8, uint32_t num_puzzles) {
-        const bool reset = (hw & 0x400000u) != 0u;
+        const bool reset = hw_reset(hw);
         const uint32_t dd = (uint32_t)((int32_t)hw >> 14) & 0xFFFF0000u;
-        const bool moved = hw >= 0x40000000u, done = (hw & 0x30000u) != 0u;
+        const bool moved = hw >= 0x40000000u, done = (hw & kHwDone) != 0u;
         if (reset) {
             const bool fb = nres >= lim;
             pid = npid;
@@ -157,10 +164,10 @@ struct TrieLane {
     template <bool CODES = true, class Rows>
     __device__ __forceinline__ int step1la(const uint32_t hw, const uint32_t a, const uint32_t an, const Rows& trow,
                                            const uint2* __restrict__ trieg, uint32_t num_puzzles) {
-        const bool reset = (hw & 0x400000u) != 0u;
+        const bool reset = hw_reset(hw);
         const uint32_t dd = (uint32_t)((int32_t)hw >> 14) & 0xFFFF0000u;
         const bool moved = hw >= 0x40000000u;
-        const bool done = (hw & 0x30000u) != 0u;
+        const bool done = (hw & kHwDone) != 0u;
         if (reset) {
             pid = npid;
             npid = next_pid(npid, num_puzzles);
@@ -173,7 +180,7 @@ struct TrieLane {
             hsb = (uint32_t)hs << 2;
             tmax = nx.w >> 17;
         }
-        nx = trow[npid];
+        nx = row4(trow, npid);
         const uint64_t xy = ((uint64_t)ry << 32) | rx;
         const uint32_t c = (uint32_t)(xy >> ((a << 4) & 0x30u));
         const uint32_t key = __builtin_amdgcn_ubfe(c, 0u, 16u) | (S & 0xFFFF0000u) | (~dd & 0x10000u);
@@ -209,13 +216,13 @@ struct TrieLane {
         return step_core<CODES>((hw & 0x40u) != 0u, hw & 0xFFFF0000u, hw >= 0x10000u, (hw & 3u) != 0u, a, trow, trie8,
                          num_puzzles);
     }
-    // the same from the W = 1 split move wave's word (sparc_move1.hpp): flag byte at bits 16-23,
-    // fwd - pop at bits 30-31 (sign-extended down to bits 16-31)
+    // the same from the W = 1 split move wave's word (sparc_move1.hpp): reset iff at-target set
+    // and done clear, done at bit 25, fwd - pop at bits 30-31 (sign-extended down to bits 16-31)
     template <bool CODES = true, class Rows>
     __device__ __forceinline__ int step1(const uint32_t hw, const uint32_t a, const Rows& trow,
                                          const uint2* __restrict__ trie8, uint32_t num_puzzles) {
-        return step_core<CODES>((hw & 0x400000u) != 0u, (uint32_t)((int32_t)hw >> 14) & 0xFFFF0000u, hw >= 0x40000000u,
-                         (hw & 0x30000u) != 0u, a, trow, trie8, num_puzzles);
+        return step_core<CODES>(hw_reset(hw), (uint32_t)((int32_t)hw >> 14) & 0xFFFF0000u,
+                                hw >= 0x40000000u, (hw & kHwDone) != 0u, a, trow, trie8, num_puzzles);
     }
 
     // reset: an autoreset step; dd = (fwd - pop) << 16 (bit 16: moved); moved = dd != 0; done:
@@ -237,12 +244,15 @@ struct TrieLane {
             hsb = (uint32_t)hs << 2;
             tmax = nx.w >> 17;
             // the row of the next reset, read here into the same registers, so nothing waits for
-            // it until that reset (at least two steps later); the empty asm keeps the uses of the
-            // old row above the read (else the compiler lands the read in temporaries and waits
-            // for it right here to copy it into nx).  MI355X, c3: 0.4003-0.4014 -> 0.3950-0.3962
-            // ms per 2,000-step launch against the read on every step (profiles/r04/ab_run2)
-            __asm__ volatile("" ::: "memory");
-            nx = trow[npid];
+            // it until that reset (at least two steps later).  MI355X, c3: 0.4003-0.4014 ->
+            // 0.3950-0.3962 ms per 2,000-step launch against the read on every step
+            // (profiles/r04/ab_run2).  The empty asm takes the values made from the old row as
+            // operands, so they exist before the read is issued, and nx is one 4-vector: with only
+            // a memory clobber the compiler landed the read in temporaries and waited for it in
+            // the branch to copy it into nx (as MoveLane1::reset_next)
+            if constexpr (CODES) __asm__ volatile("" ::"v"(rx), "v"(ry), "v"(base), "v"(S), "v"(hs), "v"(hsn) : "memory");
+            else __asm__ volatile("" ::"v"(rx), "v"(ry), "v"(base), "v"(S), "v"(hsb) : "memory");
+            nx = row4(trow, npid);
         }
         // forward move or pop on the trie: field[action] (a child, or the parent).  key has
         // bits above 15 set when the lane is off the trie or did not move, so one compare

@@ -91,6 +91,32 @@ VARIANTS = {
     }""", """        mrow = lm;
     }""")],
     # k_rollout1s without the trie wave's priority (re-checked after IOR balanced the chains)
+    # the look-ahead trie wave (step1la) on every LDS-table grid, not only on <= 64 workgroups
+    "la": [("sparc_kernels.hip", "if (lds_s && blocks <= 64) launch_s(k_rollout1s<TB, false, true, true, IOR>, d_act);",
+            "if (lds_s) launch_s(k_rollout1s<TB, false, true, true, IOR>, d_act);")],
+    # the same with the look-ahead gather only for lanes on the trie (off it, no later step takes)
+    "lamask": [("sparc_kernels.hip", "if (lds_s && blocks <= 64) launch_s(k_rollout1s<TB, false, true, true, IOR>, d_act);",
+                "if (lds_s) launch_s(k_rollout1s<TB, false, true, true, IOR>, d_act);"),
+               ("sparc_trie.hpp", """        const uint2 rec = trieg[((base + (S & 0x7FFFu)) << 2) + (an & 3u)];
+        nrx = rec.x;
+        nry = rec.y;""", """        if (S < 0x10000u) {
+            const uint2 rec = trieg[((base + (S & 0x7FFFu)) << 2) + (an & 3u)];
+            nrx = rec.x;
+            nry = rec.y;
+        }""")],
+    # only the masked gather (c2's look-ahead grids)
+    "lamask2": [("sparc_trie.hpp", """        const uint2 rec = trieg[((base + (S & 0x7FFFu)) << 2) + (an & 3u)];
+        nrx = rec.x;
+        nry = rec.y;""", """        if (S < 0x10000u) {
+            const uint2 rec = trieg[((base + (S & 0x7FFFu)) << 2) + (an & 3u)];
+            nrx = rec.x;
+            nry = rec.y;
+        }""")],
+    # k_rollout_obsw occupancy: waves per SIMD allowed by the register budget
+    "obsw6": [("sparc_kernels.hip", "__launch_bounds__(kBlockOw) __attribute__((amdgpu_waves_per_eu(4)))",
+               "__launch_bounds__(kBlockOw) __attribute__((amdgpu_waves_per_eu(6)))")],
+    "obsw8": [("sparc_kernels.hip", "__launch_bounds__(kBlockOw) __attribute__((amdgpu_waves_per_eu(4)))",
+               "__launch_bounds__(kBlockOw) __attribute__((amdgpu_waves_per_eu(8)))")],
     "noprio": [("sparc_kernels.hip", """        __builtin_amdgcn_s_setprio(1);
         TrieLane tl;""", """        TrieLane tl;""")],
     # k_rollout1r with s_memtime stamps (timing only: the stats buffer receives, per wave, role |

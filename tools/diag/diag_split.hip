@@ -20,9 +20,9 @@ struct DiagTrieLane : TrieLane {
     __device__ __forceinline__ int step1d(const uint32_t hw, const uint32_t a, const Rows& trow,
                                           const uint2* __restrict__ trie8, uint32_t num_puzzles) {
         if constexpr (G == 0) return step1<CODES>(hw, a, trow, trie8, num_puzzles);
-        const bool reset = (hw & 0x400000u) != 0u;
+        const bool reset = hw_reset(hw);
         const uint32_t dd = (uint32_t)((int32_t)hw >> 14) & 0xFFFF0000u;
-        const bool moved = hw >= 0x40000000u, done = (hw & 0x30000u) != 0u;
+        const bool moved = hw >= 0x40000000u, done = (hw & kHwDone) != 0u;
         if (reset) {
             pid = npid;
             npid = next_pid(npid, num_puzzles);
@@ -34,7 +34,7 @@ struct DiagTrieLane : TrieLane {
             hsn = -hs;
             tmax = nx.w >> 17;
         }
-        nx = trow[npid];
+        nx = row4(trow, npid);
         const uint64_t xy = ((uint64_t)ry << 32) | rx;
         const uint32_t c = (uint32_t)(xy >> ((a << 4) & 0x30u));
         const uint32_t key = __builtin_amdgcn_ubfe(c, 0u, 16u) | (S & 0xFFFF0000u) | (~dd & 0x10000u);
@@ -65,18 +65,20 @@ struct DiagTrieLane : TrieLane {
 
 
 // MoveLane1 with the autoreset variants: MV 0 the product's (divergent branch), 1 none (timing
-// only), 2 a wave-uniform branch around it (no exec save / restore when no lane resets), 3
-// branch-free selects with the next reset row read every step
+// only), 2 a wave-uniform branch around it (no exec save / restore when no lane resets), 4 the
+// branch without the next-row prefetch (timing only)
 template <bool TB, int MV>
 struct DiagMoveLane1 : MoveLane1<TB> {
     using B = MoveLane1<TB>;
-    __device__ __forceinline__ void reset_v(const Params& p, const uint4* mrow, uint32_t col_addr) {
+    __device__ __forceinline__ bool reset_v(const bool ar, const uint4* mrow, uint32_t col_addr) {
         if constexpr (MV == 0) {
-            B::reset_next(p, mrow, col_addr);
+            return B::reset_next(ar, mrow, col_addr);
         } else if constexpr (MV == 2) {
-            if (__builtin_amdgcn_ballot_w64((B::pending != 0u) & (p.autoreset == 1))) B::reset_next(p, mrow, col_addr);
-        } else if constexpr (MV == 4) {   // the branch without the next-row prefetch (timing only)
-            if ((B::pending != 0u) & (p.autoreset == 1)) {
+            if (__builtin_amdgcn_ballot_w64(B::pending & ar)) return B::reset_next(ar, mrow, col_addr);
+            return false;
+        } else if constexpr (MV == 4) {
+            const bool rs = B::pending & ar;
+            if (rs) {
                 B::e = B::rr.x & 0xFFu;
                 B::tgt = (B::rr.x >> 8) & 0xFFu;
                 B::pflags = B::rr.x >> 16;
@@ -90,48 +92,10 @@ struct DiagMoveLane1 : MoveLane1<TB> {
                     B::len = 1;
                 }
                 B::step = -1;
-                B::lv = kHwReset;
             }
-        } else if constexpr (MV == 5) {   // the next-row prefetch every step, outside the branch
-            const uint4 nx = mrow[B::rr.w];
-            if ((B::pending != 0u) & (p.autoreset == 1)) {
-                B::e = B::rr.x & 0xFFu;
-                B::tgt = (B::rr.x >> 8) & 0xFFu;
-                B::pflags = B::rr.x >> 16;
-                B::fr = ((uint64_t)B::rr.z << 32) | B::rr.y;
-                B::w = 0;
-                if constexpr (TB) {
-                    B::sp = col_addr;
-                    B::set_bks(col_addr);
-                    B::bias = 0;
-                } else {
-                    B::len = 1;
-                }
-                B::step = -1;
-                B::lv = kHwReset;
-                B::rr = nx;
-            }
-        } else if constexpr (MV == 3) {
-            const bool rs = (B::pending != 0u) & (p.autoreset == 1);
-            const uint4 nx = mrow[B::rr.w];
-            B::e = rs ? (B::rr.x & 0xFFu) : B::e;
-            B::tgt = rs ? ((B::rr.x >> 8) & 0xFFu) : B::tgt;
-            B::pflags = rs ? (B::rr.x >> 16) : B::pflags;
-            B::fr = rs ? (((uint64_t)B::rr.z << 32) | B::rr.y) : B::fr;
-            B::w = rs ? 0u : B::w;
-            if constexpr (TB) {
-                B::sp = rs ? col_addr : B::sp;
-                B::bks = rs ? 0x80000000u - col_addr - 128u + 64u * ((~(B::rr.x >> 16) >> 2) & 1u) : B::bks;
-                B::bias = rs ? 0u : B::bias;
-            } else {
-                B::len = rs ? 1u : B::len;
-            }
-            B::step = rs ? -1 : B::step;
-            B::lv = rs ? kHwReset : B::lv;
-            B::rr.x = rs ? nx.x : B::rr.x;
-            B::rr.y = rs ? nx.y : B::rr.y;
-            B::rr.z = rs ? nx.z : B::rr.z;
-            B::rr.w = rs ? nx.w : B::rr.w;
+            return rs;
+        } else {
+            return false;
         }
     }
 };
@@ -175,9 +139,7 @@ extern "C" int sparc_diag_rollout1s(void* ctx, int32_t T, const uint8_t* d_act, 
         };
         if (mv == 1) pg(std::integral_constant<int, 1>{});
         else if (mv == 2) pg(std::integral_constant<int, 2>{});
-        else if (mv == 3) pg(std::integral_constant<int, 3>{});
         else if (mv == 4) pg(std::integral_constant<int, 4>{});
-        else if (mv == 5) pg(std::integral_constant<int, 5>{});
         else pg(std::integral_constant<int, 0>{});
     };
     if (c->cfg.traceback) pick(std::true_type{});
