@@ -919,7 +919,11 @@ __global__ void __launch_bounds__(kBlock1) k_rollout1(Params p, int32_t T, const
 // host runs any tail (and other pools) through k_rollout1.  The state after the launch is the same SoA record (the trie wave hands its
 // final trie state and counters to the move wave through LDS before the store).
 constexpr int kBlock1s = 768;
-constexpr size_t kS_Act = 0;                          // actions [3 tiles][16][64] (trie wave)
+// steps per LDS read group of the move and trie waves: a group's inputs (target positions;
+// hand-over words and actions) are read together and waited for once
+constexpr int kGroup1s = 4;
+static_assert(kTile % kGroup1s == 0, "k_rollout1s read groups");
+constexpr size_t kS_Act = 0;                          // actions << 4 [3 tiles][16][64] (trie wave)
 constexpr size_t kS_Pos = kS_Act + 3 * kTile * 64;    // target window positions [3 tiles][16][64] (move wave)
 constexpr size_t kS_Rew = kS_Pos + 3 * kTile * 64;    // reward ring [64 steps][64]
 constexpr size_t kS_FH = kS_Rew + kRing * 64;         // hand-over ring [64 steps][64] u32
@@ -1071,7 +1075,9 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
                 v.z = clamp_actions4(v.z);
                 v.w = clamp_actions4(v.w);
                 const size_t o = io * kS_Pair + (k % 3) * (kTile * 64) + r * 64 + c;
-                *reinterpret_cast<u32x4*>(smem + kS_Act + o) = v;
+                // the trie wave's copy as action << 4 (bytes <= 4: no carry between bytes), the
+                // shift of its record field (TrieLane::walk1)
+                *reinterpret_cast<u32x4*>(smem + kS_Act + o) = u32x4{v.x << 4, v.y << 4, v.z << 4, v.w << 4};
                 // the move wave's input: each action's target window position (byte a of
                 // nbr_pos; P, the agent's own never-free bit, for the illegal action 4)
                 u32x4 q;
@@ -1165,20 +1171,20 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
             const uint8_t* tp = pb + kS_Pos + (k % 3) * (kTile * 64) + lane;
             uint8_t* ta = pb + kS_Act + (k % 3) * (kTile * 64) + lane;
 #pragma unroll 1
-            for (int g = 0; g < kTile; g += 4) {
-                uint32_t pv[4];
+            for (int g = 0; g < kTile; g += kGroup1s) {
+                uint32_t pv[kGroup1s];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
+                for (int j = 0; j < kGroup1s; ++j) {
                     if constexpr (RAND) {
                         const uint32_t a = uint_rand_action(seed, gid, t0 + (uint64_t)(k * kTile + g + j));
-                        ta[(g + j) * 64] = (uint8_t)a;
+                        ta[(g + j) * 64] = (uint8_t)(a << 4);   // the trie wave's action << 4
                         pv[j] = __builtin_amdgcn_ubfe(p.nbr_pos, a << 3, 8u);
                     } else {
                         pv[j] = tp[(g + j) * 64];
                     }
                 }
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
+                for (int j = 0; j < kGroup1s; ++j) {
                     const uint32_t row = (uint32_t)(k * kTile + g + j) & (kRing - 1);
                     bool rs;
                     if constexpr (LDS_TABLE) rs = m.reset_next(ar, mrow, col_addr);
@@ -1238,19 +1244,19 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
             // the last tile it is stale, and that look-ahead is never used)
             const uint32_t a_next = LA ? pb[kS_Act + (k % 3) * (kTile * 64) + lane] : 0u;
 #pragma unroll 1
-            for (int g = 0; g < kTile; g += 4) {
-                // the group's 4 hand-over words and actions (LA: and the next one) first (one LDS
-                // wait), then its 4 steps
+            for (int g = 0; g < kTile; g += kGroup1s) {
+                // the group's hand-over words and actions (LA: and the next one) first (one LDS
+                // wait), then its steps
                 const uint32_t row0 = (uint32_t)((k - 1) * kTile + g) & (kRing - 1);
-                uint32_t hb[4], av[5];
+                uint32_t hb[kGroup1s], av[kGroup1s + 1];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
+                for (int j = 0; j < kGroup1s; ++j) {
                     hb[j] = th[(row0 + j) * 64];
                     av[j] = ta[(g + j) * 64];
                 }
-                if constexpr (LA) av[4] = g + 4 < kTile ? (uint32_t)ta[(g + 4) * 64] : a_next;
+                if constexpr (LA) av[kGroup1s] = g + kGroup1s < kTile ? (uint32_t)ta[(g + kGroup1s) * 64] : a_next;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
+                for (int j = 0; j < kGroup1s; ++j) {
                     int code;
                     if constexpr (LA) code = tl.step1la<!IOR>(hb[j], av[j], av[j + 1], trow, p.tab.trieg, NP);
                     else if constexpr (LDS_TABLE) code = tl.step1<!IOR>(hb[j], av[j], trow, p.tab.trie8, NP);
@@ -2283,28 +2289,47 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
     for (size_t q = 0; q < P; ++q)
         if (((t->info[4 * q + 1] >> 16) & 2u) && (t->info[4 * q + 3] & 0xFFFFu) > 0x7FFFu) small = false;
     if (small) {
-        std::vector<uint2> t8(nn, make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu));
+        // each puzzle's records start on a 128-B line (16 records; rootless puzzles: base 0): in
+        // breadth-first order the root and the nodes near it, which most walks never leave,
+        // share ONE line per puzzle instead of straddling two, so pools whose tries outgrow an
+        // XCD's L2 refill fewer lines (the relative node indices, and so the env state, are
+        // unchanged; only the split tables move)
+        std::vector<size_t> b8(P, 0);
+        size_t nn8 = 0;
+        for (size_t q = 0; q < P; ++q) {
+            const uint32_t* inf = t->info + 4 * q;
+            if (!((inf[1] >> 16) & 2u)) continue;
+            nn8 = (nn8 + 15u) & ~(size_t)15u;
+            b8[q] = nn8;
+            nn8 += inf[3] & 0xFFFFu;
+        }
+        nn8 = std::max<size_t>(nn8, 1);
+        if (W == 1) {   // Env<1> (k_step, k_rollout1) reads trie8 at row1.y too
+            for (size_t q = 0; q < P; ++q) row1[q].y = (uint32_t)b8[q];
+            HIPCHK(c, hipMemcpy(c->t_row1, row1.data(), sizeof(uint4) * P, hipMemcpyHostToDevice));
+        }
+        std::vector<uint2> t8(nn8, make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu));
         auto packed = [&](size_t base, uint32_t k) {   // node k of a puzzle as index | terminal << 15
             return k | (((t->trie[4 * (base + k) + 2] >> 16) & 1u) << 15);
         };
         for (size_t q = 0; q < P; ++q) {
             const uint32_t* inf = t->info + 4 * q;
             if (!((inf[1] >> 16) & 2u)) continue;
-            const size_t base = inf[2];
+            const size_t base = inf[2], bq = b8[q];
             const uint32_t cnt = inf[3] & 0xFFFFu;
             for (uint32_t k = 0; k < cnt; ++k) {
                 const uint32_t* r = t->trie + 4 * (base + k);
                 const uint32_t ch[4] = {r[0] & 0xFFFFu, r[0] >> 16, r[1] & 0xFFFFu, r[1] >> 16};
                 uint32_t f[4];
                 for (int d = 0; d < 4; ++d) f[d] = ch[d] == kNone ? 0xFFFFu : packed(base, ch[d]);
-                t8[base + k] = make_uint2(f[0] | (f[1] << 16), f[2] | (f[3] << 16));
+                t8[bq + k] = make_uint2(f[0] | (f[1] << 16), f[2] | (f[3] << 16));
             }
             for (uint32_t k = 0; k < cnt; ++k) {           // parents, after every child field
                 const uint32_t* r = t->trie + 4 * (base + k);
                 const uint32_t ch[4] = {r[0] & 0xFFFFu, r[0] >> 16, r[1] & 0xFFFFu, r[1] >> 16};
                 for (uint32_t d = 0; d < 4; ++d) {
                     if (ch[d] == kNone) continue;
-                    uint2& cr = t8[base + ch[d]];
+                    uint2& cr = t8[bq + ch[d]];
                     const uint32_t back = d ^ 2u, sh = (back & 1u) * 16u;
                     uint32_t& w = back < 2 ? cr.x : cr.y;
                     w = (w & ~(0xFFFFu << sh)) | (packed(base, k) << sh);
@@ -2316,25 +2341,25 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
             const uint32_t* inf = t->info + 4 * q;
             const uint32_t fl = (dinfo[q].y >> 16) & 0xFFFFu;
             const uint32_t cnt = inf[3] & 0xFFFFu;
-            const uint2 rr = (fl & 2u) ? t8[inf[2]] : make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+            const uint2 rr = (fl & 2u) ? t8[b8[q]] : make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
             // flags as row1: bit0 solutions, bit1 root valid, bit3 root terminal
             const uint32_t tf = (fl & 3u) | (((dinfo[q].y >> 19) & 1u) << 3);
             const uint32_t rootS = (tf & 2u) ? ((tf >> 3) & 1u) << 15 : 0x10000u;
-            trow[q] = make_uint4(rr.x, rr.y, inf[2], rootS | ((tf & 1u) << 14) | ((cnt ? cnt - 1u : 0u) << 17));
+            trow[q] = make_uint4(rr.x, rr.y, (uint32_t)b8[q], rootS | ((tf & 1u) << 14) | ((cnt ? cnt - 1u : 0u) << 17));
             // W = 1 move row: row word, reset board, and the puzzle the autoreset after it loads
             if (W == 1) mrow[q] = make_uint4(row1[q].x, (uint32_t)init[q], (uint32_t)(init[q] >> 32),
                                              q + 1 == P ? 0u : (uint32_t)q + 1u);
         }
-        HIPCHK(c, hipMalloc(&c->t_trie8, sizeof(uint2) * nn));
-        HIPCHK(c, hipMemcpy(c->t_trie8, t8.data(), sizeof(uint2) * nn, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMalloc(&c->t_trie8, sizeof(uint2) * nn8));
+        HIPCHK(c, hipMemcpy(c->t_trie8, t8.data(), sizeof(uint2) * nn8, hipMemcpyHostToDevice));
         // look-ahead records (TrieLane::step1la): entry 4k + d = the record of node k's field-d
         // node (child, or the parent in the back direction), all ones where the field is empty;
         // at least 4 entries, so that a rootless puzzle's lane (base 0, node 0) reads in bounds
-        std::vector<uint2> tg(4 * std::max<size_t>(nn, 1), make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu));
+        std::vector<uint2> tg(4 * nn8, make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu));
         for (size_t q = 0; q < P; ++q) {
             const uint32_t* inf = t->info + 4 * q;
             if (!((inf[1] >> 16) & 2u)) continue;
-            const size_t base = inf[2];
+            const size_t base = b8[q];
             const uint32_t cnt = inf[3] & 0xFFFFu;
             for (uint32_t k = 0; k < cnt; ++k) {
                 const uint2 r = t8[base + k];

@@ -83,7 +83,10 @@ struct MoveLane1 {
     uint32_t tgt = 0, pflags = 0, len = 1;
     bool pending = false;                 // the last step was done (not an autoreset step)
     int32_t step = 0;
-    uint32_t sp = 0, bks = 0, bias = 0;   // traceback: stack slot len-1 (LDS byte address), rule bias
+    // traceback: sq = the LDS byte address of stack slot len-3 (slot len-1 is sq + 128: the step
+    // writes it through the instruction's offset field and reads slot len-3 with no address add),
+    // the rule bias and its constant
+    uint32_t sq = 0, bks = 0, bias = 0;
     uint32_t rp = 0, pnr = 0;             // traceback: back position of the last move / the one before
     uint4 rr = {0u, 0u, 0u, 0u};          // the next autoreset's move row: row word, free board, the puzzle after it
     // global rows (k_rollout1s<…, LDS_TABLE = false>, row_slots below): the next autoreset's trie
@@ -102,8 +105,8 @@ struct MoveLane1 {
     __device__ __forceinline__ static uint32_t lds_addr(const uint8_t* g) { return (uint32_t)(uintptr_t)(lds_u8*)g; }
 
     __device__ __forceinline__ void set_bks(uint32_t col_addr) {
-        // (sp + bks) >> 31 = len >= 3, or len == 2 and the start is open (pflags bit 2 clear)
-        bks = 0x80000000u - col_addr - 128u + 64u * ((~pflags >> 2) & 1u);
+        // (sq + bks) >> 31 = len >= 3, or len == 2 and the start is open (pflags bit 2 clear)
+        bks = 0x80000000u - col_addr + 64u * ((~pflags >> 2) & 1u);
     }
     __device__ __forceinline__ void prefetch_reset(const uint4* mrow, uint32_t q) {
         rr = mrow[q];
@@ -126,7 +129,7 @@ struct MoveLane1 {
             fr = ((uint64_t)rr.z << 32) | rr.y;
             w = 0;
             if constexpr (TB) {
-                sp = col_addr;   // len = 1
+                sq = col_addr - 128u;   // len = 1
                 set_bks(col_addr);
                 bias = 0;
             } else {
@@ -160,7 +163,7 @@ struct MoveLane1 {
             fr = ((uint64_t)rg.z << 32) | rg.y;
             w = 0;
             if constexpr (TB) {
-                sp = col_addr;
+                sq = col_addr - 128u;
                 set_bks(col_addr);
                 bias = 0;
             } else {
@@ -202,10 +205,10 @@ struct MoveLane1 {
         const int32_t dl = (int32_t)fwd - (int32_t)pop;
         if constexpr (TB) {
             const uint32_t arp = 2u * P - pos;         // back position of this move
-            *lds_byte(sp) = (uint8_t)arp;              // slot len-1: the new top if fwd
+            *lds_byte(sq + 128u) = (uint8_t)arp;       // slot len-1: the new top if fwd
             rp = fwd ? arp : (pop ? pnr : rp);
-            sp += (uint32_t)dl << 6;
-            bias = (sp + bks) >> 31;
+            sq += (uint32_t)dl << 6;
+            bias = (sq + bks) >> 31;
         } else {
             len += fwd;
         }
@@ -219,7 +222,7 @@ struct MoveLane1 {
         // an autoreset step is never done (w = 0 before it: lw was 0) and reports at-target
         pending = done & !rs;
         // the move before the last (slot len-3 after the step), for the next pop
-        if constexpr (TB) pnr = *lds_byte(sp - 128u);
+        if constexpr (TB) pnr = *lds_byte(sq);
         return ((uint32_t)dl << 30) | ((at_tgt | rs) ? kHwTgt : 0u) | (pending ? kHwDone : 0u) | lw;
     }
 
@@ -246,11 +249,11 @@ struct MoveLane1 {
                 const uint32_t a = (uint32_t)(((k < 32 ? lo : hi) >> ((k & 31u) * 2u)) & 3u);
                 col[k * 64u] = (uint8_t)dir_pos1(a ^ 2u, P);
             }
-            sp = col_addr + (len - 1u) * 64u;
+            sq = col_addr + (len - 1u) * 64u - 128u;
             set_bks(col_addr);
-            bias = (sp + bks) >> 31;
+            bias = (sq + bks) >> 31;
             rp = len >= 2 ? col[(len - 2u) * 64u] : 0u;
-            pnr = *lds_byte(sp - 128u);
+            pnr = *lds_byte(sq);
         }
     }
 
@@ -266,7 +269,7 @@ struct MoveLane1 {
         const uint64_t vis = ((~fr) >> P & open) | (1ull << sb);
         s.vis[i] = vis;
         if constexpr (TB) {
-            len = (sp - col_addr) / 64u + 1u;
+            len = (sq + 128u - col_addr) / 64u + 1u;
             uint64_t lo = 0, hi = 0;
             for (uint32_t k = 0; k + 1 < len; ++k) {
                 const uint64_t v = (uint64_t)(pos_dir1(col[k * 64u], P) ^ 2u) << ((k & 31u) * 2u);

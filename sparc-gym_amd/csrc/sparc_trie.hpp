@@ -101,11 +101,9 @@ struct TrieLane {
         cA = nres;
     }
     template <bool CODES, uint32_t SLOTS, uint32_t STRIDE, class Rows>
-    __device__ __forceinline__ int step1s(const uint32_t hw, const uint32_t a, const Rows& trow,
+    __device__ __forceinline__ int step1s(const uint32_t hw, const uint32_t a16, const Rows& trow,
                                           const uint2* __restrict__ trie8, uint32_t num_puzzles) {
         const bool reset = hw_reset(hw);
-        const uint32_t dd = (uint32_t)((int32_t)hw >> 14) & 0xFFFF0000u;
-        const bool moved = hw >= 0x40000000u, done = (hw & kHwDone) != 0u;
         if (reset) {
             const bool fb = nres >= lim;
             pid = npid;
@@ -114,7 +112,8 @@ struct TrieLane {
             nres += 1u;
             if (fb) apply_row(ld_off(trow, pid << 4));   // the move wave wrote its spare slot: the L2 row
         }
-        const int code = step_core<CODES>(false, dd, moved, done, a, trow, trie8, num_puzzles);
+        if (walk1(hw, a16)) gather(trie8);
+        const int code = finish<CODES>(hw >= 0x40000000u, (hw & kHwDone) != 0u);
         // the next reset's slot, in case that reset falls in this tile (at least two steps later:
         // waited for with the LDS reads of a later step)
         if (reset) slot_read(SLOTS, STRIDE);
@@ -152,23 +151,20 @@ struct TrieLane {
         Oneg = (last_hw_done != 0u && (S >> 15) == 1u) ? 0 : -100;
     }
 
-    // after load(): the first step's look-ahead record (a0: its action)
-    __device__ __forceinline__ void prime(const uint32_t a0, const uint2* __restrict__ trieg) {
+    // after load(): the first step's look-ahead record (a016: its action << 4)
+    __device__ __forceinline__ void prime(const uint32_t a016, const uint2* __restrict__ trieg) {
         const uint32_t node = S & 0x7FFFu;
-        const uint2 rec = trieg[((base + (node < tmax ? node : tmax)) << 2) + (a0 & 3u)];
+        const uint2 rec = trieg[((base + (node < tmax ? node : tmax)) << 2) + __builtin_amdgcn_ubfe(a016, 4u, 2u)];
         nrx = rec.x;
         nry = rec.y;
     }
 
-    // step1 (the W = 1 move wave's word) with the look-ahead record; an: the next step's action
+    // step1 (the W = 1 move wave's word, a16 = action << 4) with the look-ahead record; an16: the
+    // next step's action << 4
     template <bool CODES = true, class Rows>
-    __device__ __forceinline__ int step1la(const uint32_t hw, const uint32_t a, const uint32_t an, const Rows& trow,
+    __device__ __forceinline__ int step1la(const uint32_t hw, const uint32_t a16, const uint32_t an16, const Rows& trow,
                                            const uint2* __restrict__ trieg, uint32_t num_puzzles) {
-        const bool reset = hw_reset(hw);
-        const uint32_t dd = (uint32_t)((int32_t)hw >> 14) & 0xFFFF0000u;
-        const bool moved = hw >= 0x40000000u;
-        const bool done = (hw & kHwDone) != 0u;
-        if (reset) {
+        if (hw_reset(hw)) {
             pid = npid;
             npid = next_pid(npid, num_puzzles);
             rx = nx.x;
@@ -181,31 +177,19 @@ struct TrieLane {
             tmax = nx.w >> 17;
         }
         nx = row4(trow, npid);
-        const uint64_t xy = ((uint64_t)ry << 32) | rx;
-        const uint32_t c = (uint32_t)(xy >> ((a << 4) & 0x30u));
-        const uint32_t key = __builtin_amdgcn_ubfe(c, 0u, 16u) | (S & 0xFFFF0000u) | (~dd & 0x10000u);
-        const bool take = key < 0xFFFFu;
-        S = take ? key : S + dd;
+        const bool take = walk1(hw, a16);
         // the new node's record arrived with the previous step's look-ahead gather (a reset
-        // step never takes: dd = 0)
+        // step never takes: it does not move)
         rx = take ? nrx : rx;
         ry = take ? nry : ry;
         // the next step's: field[an] of the node now current (on or off the trie, the node is
         // one of this puzzle's: in bounds; used only if that step takes).  Unconditional: an
-        // exec-masked gather for on-trie lanes only measured slower here (c2: 0.346 vs 0.337 ms)
-        const uint2 rec = trieg[((base + (S & 0x7FFFu)) << 2) + (an & 3u)];
+        // exec-masked gather for on-trie lanes only measured slower here (c2: 0.346 vs 0.337 ms;
+        // round 5: 0.2863 vs 0.3215 ms, profiles/r05/ab_handover)
+        const uint2 rec = trieg[((base + (S & 0x7FFFu)) << 2) + __builtin_amdgcn_ubfe(an16, 4u, 2u)];
         nrx = rec.x;
         nry = rec.y;
-        const uint32_t x = S >> 15;
-        if constexpr (!CODES) return (int)class_byte(x);
-        const int cd = x == 1u ? 100 : Oneg;
-        const int cm = moved ? (x < 2u ? hs : hsn) : 0;
-        const int code = done ? cd : cm;
-        Oneg = done ? (cd < 0 ? cd : 0) : -100;
-        acc_x += code;
-        acc_y += (uint32_t)done;
-        acc_z += (uint32_t)(code == 100);
-        return code;
+        return finish<CODES>(hw >= 0x40000000u, (hw & kHwDone) != 0u);
     }
 
     // one env-step from its hand-over word (layout above) and action; returns the reward code
@@ -216,13 +200,15 @@ struct TrieLane {
         return step_core<CODES>((hw & 0x40u) != 0u, hw & 0xFFFF0000u, hw >= 0x10000u, (hw & 3u) != 0u, a, trow, trie8,
                          num_puzzles);
     }
-    // the same from the W = 1 split move wave's word (sparc_move1.hpp): reset iff at-target set
-    // and done clear, done at bit 25, fwd - pop at bits 30-31 (sign-extended down to bits 16-31)
+    // the same from the W = 1 split move wave's word (sparc_move1.hpp: reset iff at-target set and
+    // done clear, done at bit 25, fwd - pop at bits 30-31) and a16 = the action << 4 (the I/O wave
+    // stores the trie wave's actions that way, k_rollout1s)
     template <bool CODES = true, class Rows>
-    __device__ __forceinline__ int step1(const uint32_t hw, const uint32_t a, const Rows& trow,
+    __device__ __forceinline__ int step1(const uint32_t hw, const uint32_t a16, const Rows& trow,
                                          const uint2* __restrict__ trie8, uint32_t num_puzzles) {
-        return step_core<CODES>(hw_reset(hw), (uint32_t)((int32_t)hw >> 14) & 0xFFFF0000u,
-                                hw >= 0x40000000u, (hw & kHwDone) != 0u, a, trow, trie8, num_puzzles);
+        if (hw_reset(hw)) reset_from_nx<CODES>(trow, num_puzzles);
+        if (walk1(hw, a16)) gather(trie8);
+        return finish<CODES>(hw >= 0x40000000u, (hw & kHwDone) != 0u);
     }
 
     // reset: an autoreset step; dd = (fwd - pop) << 16 (bit 16: moved); moved = dd != 0; done:
@@ -232,28 +218,7 @@ struct TrieLane {
     __device__ __forceinline__ int step_core(const bool reset, const uint32_t dd, const bool moved, const bool done,
                                              const uint32_t a, const Rows& trow, const uint2* __restrict__ trie8,
                                              uint32_t num_puzzles) {
-        if (reset) {   // autoreset step: the next puzzle's rows and its trie root
-            pid = npid;
-            npid = next_pid(npid, num_puzzles);
-            rx = nx.x;
-            ry = nx.y;
-            base = nx.z;
-            S = nx.w & 0x18000u;
-            hs = (int32_t)((nx.w >> 14) & 1u);
-            hsn = -hs;
-            hsb = (uint32_t)hs << 2;
-            tmax = nx.w >> 17;
-            // the row of the next reset, read here into the same registers, so nothing waits for
-            // it until that reset (at least two steps later).  MI355X, c3: 0.4003-0.4014 ->
-            // 0.3950-0.3962 ms per 2,000-step launch against the read on every step
-            // (profiles/r04/ab_run2).  The empty asm takes the values made from the old row as
-            // operands, so they exist before the read is issued, and nx is one 4-vector: with only
-            // a memory clobber the compiler landed the read in temporaries and waited for it in
-            // the branch to copy it into nx (as MoveLane1::reset_next)
-            if constexpr (CODES) __asm__ volatile("" ::"v"(rx), "v"(ry), "v"(base), "v"(S), "v"(hs), "v"(hsn) : "memory");
-            else __asm__ volatile("" ::"v"(rx), "v"(ry), "v"(base), "v"(S), "v"(hsb) : "memory");
-            nx = row4(trow, npid);
-        }
+        if (reset) reset_from_nx<CODES>(trow, num_puzzles);
         // forward move or pop on the trie: field[action] (a child, or the parent).  key has
         // bits above 15 set when the lane is off the trie or did not move, so one compare
         // decides; off the trie (or without a child) the move counts the depth instead.
@@ -262,17 +227,64 @@ struct TrieLane {
         const uint32_t key = __builtin_amdgcn_ubfe(c, 0u, 16u) | (S & 0xFFFF0000u) | (~dd & 0x10000u);
         const bool take = key < 0xFFFFu;
         S = take ? key : S + dd;
-        // the record changes only with the node (exec-masked gather; a random walk is off the
-        // trie on most steps).  Every field of a record holds a node of the same puzzle
-        // (validated by sparc_load_puzzles), so no clamp here; load() clamps the stored node.
-        if (take) {
-            const uint2 rec = ld_off(trie8, (base + (S & 0x7FFFu)) << 3);
-            rx = rec.x;
-            ry = rec.y;
-        }
-        // reward code: done: +100 on a solution, else Oneg; otherwise +-1 when moved on a
-        // puzzle with solutions (on / off the trie), else 0 (an autoreset step neither moves
-        // nor is done)
+        if (take) gather(trie8);
+        return finish<CODES>(moved, done);
+    }
+
+    // the W = 1 transition (step_core's, from the hand-over word itself): not moved is bit 30 of
+    // the word clear (fwd - pop = 0), which keeps key above 0xFFFF as bit 16 does there, and the
+    // depth step is (fwd - pop) << 16 from one arithmetic shift: field / key / depth in 8
+    // instructions against 11 (the extraction of dd and of the not-moved bit)
+    __device__ __forceinline__ bool walk1(const uint32_t hw, const uint32_t a16) {
+        const uint64_t xy = ((uint64_t)ry << 32) | rx;
+        const uint32_t c = (uint32_t)(xy >> (a16 & 63u));           // a16 & 15 == 0: field a16 / 16
+        // field | S's depth half: one v_perm_b32 (the compiler's and / and / or3 took three)
+        const uint32_t key = __builtin_amdgcn_perm(S, c, 0x07060100u) | (~hw & 0x40000000u);
+        const bool take = key < 0xFFFFu;
+        // fwd - pop by a signed field extract, shifted and added in one v_lshl_add_u32 (written
+        // plainly, the compiler rewrote (hw >> 30) << 16 into a shift, a mask and an add)
+        const int32_t dl = __builtin_amdgcn_sbfe((int32_t)hw, 30u, 2u);
+        uint32_t Sm;
+        asm("v_lshl_add_u32 %0, %1, 16, %2" : "=v"(Sm) : "v"(dl), "v"(S));
+        S = take ? key : Sm;
+        return take;
+    }
+    // the record changes only with the node (exec-masked gather; a random walk is off the trie on
+    // most steps).  Every field of a record holds a node of the same puzzle (validated by
+    // sparc_load_puzzles), so no clamp here; load() clamps the stored node.
+    __device__ __forceinline__ void gather(const uint2* __restrict__ trie8) {
+        const uint2 rec = ld_off(trie8, (base + (S & 0x7FFFu)) << 3);
+        rx = rec.x;
+        ry = rec.y;
+    }
+    // autoreset step: the next puzzle's rows and its trie root
+    template <bool CODES, class Rows>
+    __device__ __forceinline__ void reset_from_nx(const Rows& trow, uint32_t num_puzzles) {
+        pid = npid;
+        npid = next_pid(npid, num_puzzles);
+        rx = nx.x;
+        ry = nx.y;
+        base = nx.z;
+        S = nx.w & 0x18000u;
+        hs = (int32_t)((nx.w >> 14) & 1u);
+        hsn = -hs;
+        hsb = (uint32_t)hs << 2;
+        tmax = nx.w >> 17;
+        // the row of the next reset, read here into the same registers, so nothing waits for it
+        // until that reset (at least two steps later).  MI355X, c3: 0.4003-0.4014 -> 0.3950-0.3962
+        // ms per 2,000-step launch against the read on every step (profiles/r04/ab_run2).  The
+        // empty asm takes the values made from the old row as operands, so they exist before the
+        // read is issued, and nx is one 4-vector: with only a memory clobber the compiler landed
+        // the read in temporaries and waited for it in the branch to copy it into nx (as
+        // MoveLane1::reset_next; round 5: c3 -4.3 % with the hand-over word below, c2 -6.8 %)
+        if constexpr (CODES) __asm__ volatile("" ::"v"(rx), "v"(ry), "v"(base), "v"(S), "v"(hs), "v"(hsn) : "memory");
+        else __asm__ volatile("" ::"v"(rx), "v"(ry), "v"(base), "v"(S), "v"(hsb) : "memory");
+        nx = row4(trow, npid);
+    }
+    // reward code: done: +100 on a solution, else Oneg; otherwise +-1 when moved on a puzzle with
+    // solutions (on / off the trie), else 0 (an autoreset step neither moves nor is done)
+    template <bool CODES>
+    __device__ __forceinline__ int finish(const bool moved, const bool done) {
         const uint32_t x = S >> 15;                            // 0 on, 1 on a solution, >= 2 off
         if constexpr (!CODES) return (int)class_byte(x);
         const int cd = x == 1u ? 100 : Oneg;

@@ -117,6 +117,24 @@ VARIANTS = {
                "__launch_bounds__(kBlockOw) __attribute__((amdgpu_waves_per_eu(6)))")],
     "obsw8": [("sparc_kernels.hip", "__launch_bounds__(kBlockOw) __attribute__((amdgpu_waves_per_eu(4)))",
                "__launch_bounds__(kBlockOw) __attribute__((amdgpu_waves_per_eu(8)))")],
+    # k_rollout1s: trie wave at priority 2, move wave at 1, I/O waves at 0 (the I/O waves yield)
+    "prio21": [("sparc_kernels.hip", """        __builtin_amdgcn_s_setprio(1);
+        TrieLane tl;""", """        __builtin_amdgcn_s_setprio(2);
+        TrieLane tl;"""),
+               ("sparc_kernels.hip", """    if (wv < 4) {                                                // ---- move waves
+        MoveLane1<TB> m;""", """    if (wv < 4) {                                                // ---- move waves
+        __builtin_amdgcn_s_setprio(1);
+        MoveLane1<TB> m;""")],
+    # the same with the move and trie waves at 1 (only the I/O waves yield)
+    "prio11": [("sparc_kernels.hip", """    if (wv < 4) {                                                // ---- move waves
+        MoveLane1<TB> m;""", """    if (wv < 4) {                                                // ---- move waves
+        __builtin_amdgcn_s_setprio(1);
+        MoveLane1<TB> m;""")],
+    # the split tables without the 128-B line alignment of each puzzle's trie records
+    "noalign": [("sparc_kernels.hip", "            nn8 = (nn8 + 15u) & ~(size_t)15u;\n", "")],
+    # k_rollout1s: the move and trie waves read a whole 16-step tile's inputs at once
+    "group16": [("sparc_kernels.hip", "constexpr int kGroup1s = 4;", "constexpr int kGroup1s = 16;")],
+    "group8": [("sparc_kernels.hip", "constexpr int kGroup1s = 4;", "constexpr int kGroup1s = 8;")],
     "noprio": [("sparc_kernels.hip", """        __builtin_amdgcn_s_setprio(1);
         TrieLane tl;""", """        TrieLane tl;""")],
     # k_rollout1r with s_memtime stamps (timing only: the stats buffer receives, per wave, role |

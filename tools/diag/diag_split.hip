@@ -36,7 +36,7 @@ struct DiagTrieLane : TrieLane {
         }
         nx = row4(trow, npid);
         const uint64_t xy = ((uint64_t)ry << 32) | rx;
-        const uint32_t c = (uint32_t)(xy >> ((a << 4) & 0x30u));
+        const uint32_t c = (uint32_t)(xy >> (a & 0x30u));   // a: action << 4 (k_rollout1s)
         const uint32_t key = __builtin_amdgcn_ubfe(c, 0u, 16u) | (S & 0xFFFF0000u) | (~dd & 0x10000u);
         const bool take = key < 0xFFFFu;
         S = take ? key : S + dd;
@@ -85,7 +85,7 @@ struct DiagMoveLane1 : MoveLane1<TB> {
                 B::fr = ((uint64_t)B::rr.z << 32) | B::rr.y;
                 B::w = 0;
                 if constexpr (TB) {
-                    B::sp = col_addr;
+                    B::sq = col_addr - 128u;
                     B::set_bks(col_addr);
                     B::bias = 0;
                 } else {
