@@ -571,9 +571,13 @@ def main():
         kernel = "k_rollout1s" if n % 256 == 0 and chunk >= 16 else "k_rollout1"
     elif not obs and n % 256 == 0 and chunk >= 16:
         kernel = "k_rolloutWs"   # the multi-word split kernel (when the pool fits its LDS layout)
+    elif obs:
+        kernel = "k_rollout_obsw"   # the 'new' planes by writer waves (256-env workgroups)
     else:
         kernel = "k_rollout"
     workload = f"{args.config}_{args.mode}_n{n}_chunk{chunk if args.mode == 'rollout' else 1}"
+    if args.puzzles != 1024:   # the counters of another pool size are recorded under their own key
+        workload += f"_p{args.puzzles}"
     pmc = load_traffic(workload, kernel)
     traffic = pmc["bytes"] if pmc else None
     issue = None
