@@ -569,8 +569,9 @@ def test_step_gym_action_types_and_outputs(on_gpu):
 
 @pytest.mark.parametrize("name,tb,n", [("mixed_5_11", True, 4096), ("7x7_full", False, 1001), ("15x15", True, 300)])
 def test_rollout_obs_writer_waves_equal_inline(on_gpu, name, tb, n):
-    """rollout(obs=True) runs k_rollout_obsw (compute waves stage the boards, a writer wave per
-    256 envs streams the planes); the per-wave kernel that writes its own planes
+    """rollout(obs=True) runs k_rollout_obsw (compute waves stage the boards, four writer waves
+    per 256 envs stream the planes: bit streams on the multi-word pools, the LUT on 7x7); the
+    per-wave kernel that writes its own planes
     (sparc_set_variant SPARC_VARIANT_OBS_INLINE) gives identical planes, codes, flags, stats and
     state, with file actions and with the in-kernel random actions, over two launches."""
     from sparc_gym_amd import SPaRCVecEnv
