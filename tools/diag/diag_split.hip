@@ -115,8 +115,10 @@ extern "C" int sparc_diag_rollout1s(void* ctx, int32_t T, const uint8_t* d_act, 
         return fail(c, SPARC_E_INVALID, "diag: W = 1, whole workgroups, whole tiles, all buffers");
     const Params p = make_params(c);
     if (!split1_pitch_ok(p.pitch)) return fail(c, SPARC_E_INVALID, "diag: pitch outside 3..9");
-    const size_t shm = kS_Base + split_table_bytes(c->num_puzzles);
-    if (shm > kMaxDynLds) return fail(c, SPARC_E_INVALID, "diag: table does not fit LDS");
+    // pools past the LDS row budget: the global-row kernel (row slots), product waves only
+    const bool lds = kS_Base + split_table_bytes(c->num_puzzles) <= kMaxDynLds;
+    const size_t shm = kS_Base + (lds ? split_table_bytes(c->num_puzzles) : kS_SlotBytes);
+    if (!lds && variant != 0) return fail(c, SPARC_E_INVALID, "diag: global-row pools run variant 0 only");
     auto go = [&](auto kern) {
         rc = allow_big_lds(c, reinterpret_cast<const void*>(kern));
         if (rc) return;
@@ -130,6 +132,10 @@ extern "C" int sparc_diag_rollout1s(void* ctx, int32_t T, const uint8_t* d_act, 
     const int g = variant % 10, mv = variant / 10;
     auto pick = [&](auto tb) {
         constexpr bool TB = decltype(tb)::value;
+        if (!lds) {
+            go(k_rollout1s_diag<TB, false, false, 0, 0, false, true>);
+            return;
+        }
         auto pg = [&](auto mvc) {
             constexpr int MV = decltype(mvc)::value;
             if (g == 1) go(k_rollout1s_diag<TB, false, true, 1, MV, false, true>);

@@ -34,9 +34,11 @@ ap.add_argument("--chunk", type=int, default=2000)
 ap.add_argument("--launches", type=int, default=4)
 ap.add_argument("--diag-lib", default="libsparc_diag.so")
 ap.add_argument("--variant", type=int, default=0, help="trie gather: 0 global (product), 1 LDS (fake records), 2 none")
+ap.add_argument("--puzzles", type=int, default=1024, help="pool size (bench.make_pool); past 1,024 the global-row kernel")
 a = ap.parse_args()
 sizes, full, tb, obs = bench.CONFIGS[a.config]
-proc = process_puzzles(synthetic.make_puzzles(1024, seed=0, sizes=sizes, full_properties=full))
+proc = (process_puzzles(synthetic.make_puzzles(1024, seed=0, sizes=sizes, full_properties=full)) if a.puzzles == 1024
+        else bench.make_pool(a.puzzles, sizes, full))
 table = pack_table(proc)
 vec = SPaRCVecEnv(a.envs, processed=proc, table=table, traceback=tb, observation="compact")
 gid = np.arange(a.envs, dtype=np.uint64)
