@@ -335,9 +335,25 @@ def _bits_of(mask, pitch, words):
     """Boolean [X][Y] plane -> uint64 [words] bitboard (bit x*pitch + y)."""
     out = np.zeros(words, np.uint64)
     xs, ys = np.nonzero(mask)
-    for x, y in zip(xs.tolist(), ys.tolist()):
-        b = x * pitch + y
-        out[b >> 6] |= np.uint64(1) << np.uint64(b & 63)
+    if xs.size:
+        b = xs.astype(np.uint64) * np.uint64(pitch) + ys.astype(np.uint64)
+        v = np.uint64(1) << (b & np.uint64(63))
+        w = b >> np.uint64(6)
+        for k in range(words):   # distinct bits: their sum is their OR
+            out[k] = v[w == k].sum(dtype=np.uint64)
+    return out
+
+
+def _pack_planes(masks, pitch, words):
+    """Boolean [K][X][Y] planes -> uint64 [K][words] bitboards (bit x*pitch + y), all at once."""
+    K, X, Y = masks.shape
+    bi = (np.arange(X, dtype=np.uint64)[:, None] * np.uint64(pitch) + np.arange(Y, dtype=np.uint64)[None, :]).reshape(-1)
+    v = np.uint64(1) << (bi & np.uint64(63))
+    wid = bi >> np.uint64(6)
+    flat = masks.reshape(K, -1)
+    out = np.zeros((K, words), np.uint64)
+    for k in range(words):   # distinct bits: their sum is their OR
+        out[:, k] = (flat * np.where(wid == k, v, np.uint64(0))).sum(axis=1, dtype=np.uint64)
     return out
 
 
@@ -376,21 +392,22 @@ def pack_rules(puzzles, table: PuzzleTable) -> RulesTable:
         xs, ys = np.meshgrid(np.arange(X), np.arange(Y), indexing="ij")
         cells = (xs % 2 == 1) & (ys % 2 == 1)
         layer = lambda k: (np.asarray(obs[k])[:X, :Y] == 1) if k in obs else np.zeros((X, Y), bool)  # noqa: E731
-        planes[q, RP_CELLS] = _bits_of(cells, pitch, W)
-        planes[q, RP_LATTICE] = _bits_of(np.ones((X, Y), bool), pitch, W)
-        planes[q, RP_GAPS] = _bits_of(layer("gaps"), pitch, W)
-        planes[q, RP_DOTS] = _bits_of(layer("dot"), pitch, W)
+        m = np.zeros((RULE_PLANES, X, Y), bool)
+        m[RP_CELLS] = cells
+        m[RP_LATTICE] = True
+        m[RP_GAPS] = layer("gaps")
+        m[RP_DOTS] = layer("dot")
         inner = (xs >= 1) & (xs <= X - 2) & (ys >= 1) & (ys <= Y - 2)
         tri = layer("triangle") & inner & (add > 0)
         cnt = np.clip(add, 0, 7)
-        planes[q, RP_TRI] = _bits_of(tri, pitch, W)
+        m[RP_TRI] = tri
         for k in range(3):
-            planes[q, RP_TRI0 + k] = _bits_of(tri & (((cnt >> k) & 1) == 1), pitch, W)
-        planes[q, RP_STAR] = _bits_of(layer("star") & cells, pitch, W)
-        planes[q, RP_SQUARE] = _bits_of(layer("square") & cells, pitch, W)
-        planes[q, RP_COLORED] = _bits_of((color != 0) & cells, pitch, W)
+            m[RP_TRI0 + k] = tri & (((cnt >> k) & 1) == 1)
+        m[RP_STAR] = layer("star") & cells
+        m[RP_SQUARE] = layer("square") & cells
+        m[RP_COLORED] = (color != 0) & cells
         for c in range(1, 9):
-            planes[q, RP_COL1 + c - 1] = _bits_of((color == c) & cells, pitch, W)
+            m[RP_COL1 + c - 1] = (color == c) & cells
         mult = np.zeros((X, Y), np.int64)
         for k in obs:
             if k not in RULE_SKIP_LAYERS:
@@ -399,9 +416,10 @@ def pack_rules(puzzles, table: PuzzleTable) -> RulesTable:
         if mult.max(initial=0) > 7:
             raise ValueError(f"puzzle {q}: more than 7 symbol layers on one cell")
         for k in range(3):
-            planes[q, RP_M0 + k] = _bits_of(((mult >> k) & 1) == 1, pitch, W)
-        planes[q, RP_NOTFIRST] = _bits_of(ys != 0, pitch, W)
-        planes[q, RP_NOTLAST] = _bits_of(ys != Y - 1, pitch, W)
+            m[RP_M0 + k] = ((mult >> k) & 1) == 1
+        m[RP_NOTFIRST] = ys != 0
+        m[RP_NOTLAST] = ys != Y - 1
+        planes[q] = _pack_planes(m, pitch, W)   # RP_INST stays 0 here: set per instance below
         first = len(inst)
         poly = p["polyshapes"]
         if isinstance(poly, dict):
