@@ -331,19 +331,6 @@ class RulesTable:
         return [(int(dx), int(dy)) for dx, dy in self.shape_off[int(self.shape_first[s]):int(self.shape_first[s + 1])]]
 
 
-def _bits_of(mask, pitch, words):
-    """Boolean [X][Y] plane -> uint64 [words] bitboard (bit x*pitch + y)."""
-    out = np.zeros(words, np.uint64)
-    xs, ys = np.nonzero(mask)
-    if xs.size:
-        b = xs.astype(np.uint64) * np.uint64(pitch) + ys.astype(np.uint64)
-        v = np.uint64(1) << (b & np.uint64(63))
-        w = b >> np.uint64(6)
-        for k in range(words):   # distinct bits: their sum is their OR
-            out[k] = v[w == k].sum(dtype=np.uint64)
-    return out
-
-
 def _pack_planes(masks, pitch, words):
     """Boolean [K][X][Y] planes -> uint64 [K][words] bitboards (bit x*pitch + y), all at once."""
     K, X, Y = masks.shape
