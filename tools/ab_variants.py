@@ -8,6 +8,8 @@ only to locate time (never loaded by tests, smoke or bench).
     python tools/ab_variants.py [--rev REV] <variant> [<variant> ...]   (list: python tools/ab_variants.py)
 
 --rev: the sources of git revision REV instead of the working tree (ab/lib_<variant>_<REV>.so).
+Variants whose text no longer occurs in the sources are removed once their A/B is recorded
+under profiles/ (the logs and a diff of the variant stay there).
 """
 import os
 import shutil
@@ -31,35 +33,6 @@ VARIANTS = {
     # k_rollout1r audit waves do no audit at all (the step wave, rings and barriers only)
     "noaudit": [("sparc_kernels.hip", "            if (active) {\n                if (pid != pr.q) pr = puzzle_rules<1>(p, rt, pid);",
                  "            if (false) {\n                if (pid != pr.q) pr = puzzle_rules<1>(p, rt, pid);")],
-    # c3 trie wave (TrieLane::step_core): the next reset's row read inside the reset branch into
-    # the same registers (uses pinned ahead of it), not on every step
-    "trienx": [("sparc_trie.hpp", """            tmax = nx.w >> 17;
-        }
-        // the row of the next reset, read every step outside the branch: read inside it, the
-        // compiler lands it in temporaries and waits for it right there to copy it into nx
-        nx = trow[npid];""", """            tmax = nx.w >> 17;
-            __asm__ volatile("" ::: "memory");
-            nx = trow[npid];
-        }""")],
-    # c3 trie wave (TrieLane::step_core) without the reward code and counters: it hands over only
-    # the trie position class min(S >> 15, 2), the byte an I/O-wave reward stage would need (an
-    # upper bound on moving the reward selects off the trie wave; VERDICT r3 item 4, second item)
-    "notriecode": [("sparc_trie.hpp", """        const uint32_t x = S >> 15;                            // 0 on, 1 on a solution, >= 2 off
-        const int cd = x == 1u ? 100 : Oneg;
-        const int cm = moved ? (x < 2u ? hs : hsn) : 0;
-        const int code = done ? cd : cm;
-        Oneg = done ? (cd < 0 ? cd : 0) : -100;
-        acc_x += code;
-        acc_y += (uint32_t)done;
-        acc_z += (uint32_t)(code == 100);
-        return code;
-    }
-};""", """        const uint32_t x = S >> 15;
-        (void)moved;
-        (void)done;
-        return (int)(x < 2u ? x : 2u);
-    }
-};""")],
     # the W = 1 flood fill with the -y runs filled in one step too: the +y carry fill applied to the
     # bit-reversed board (v_bfrev_b32 per half), instead of one -y step per iteration
     "downfill": [("sparc_rules.hpp", """                const uint64_t up = (((a + r) ^ a) & a) | r;
@@ -70,11 +43,6 @@ VARIANTS = {
                 const uint64_t ra = rev64(a), rr = rev64(r);
                 const uint64_t dn = rev64((((ra + rr) ^ ra) & ra) | rr);
                 N.w[0] = up | dn | (r << P) | (r >> P);""")],
-    # the observation planes stored with the default cache policy instead of nontemporal
-    "obswb": [("sparc_kernels.hip", """            if (vout) __builtin_nontemporal_store(u32x4{vv[0], vv[1], vv[2], vv[3]}, reinterpret_cast<u32x4*>(vout + f));
-            if (aout) __builtin_nontemporal_store(u32x4{aa[0], aa[1], aa[2], aa[3]}, reinterpret_cast<u32x4*>(aout + f));""",
-               """            if (vout) *reinterpret_cast<u32x4*>(vout + f) = u32x4{vv[0], vv[1], vv[2], vv[3]};
-            if (aout) *reinterpret_cast<u32x4*>(aout + f) = u32x4{aa[0], aa[1], aa[2], aa[3]};""")],
     # the plane writer's piece loop unrolled twice (more stores in flight per wave)
     "obsun2": [("sparc_kernels.hip", """    const uint32_t dl = 256u / XY, dc = 256u - dl * XY;   // a 64-piece stride in envs / cells
     for (; f < total; f += 256u) {""", """    const uint32_t dl = 256u / XY, dc = 256u - dl * XY;   // a 64-piece stride in envs / cells
@@ -94,24 +62,6 @@ VARIANTS = {
     # the look-ahead trie wave (step1la) on every LDS-table grid, not only on <= 64 workgroups
     "la": [("sparc_kernels.hip", "if (lds_s && blocks <= 64) launch_s(k_rollout1s<TB, false, true, true, IOR>, d_act);",
             "if (lds_s) launch_s(k_rollout1s<TB, false, true, true, IOR>, d_act);")],
-    # the same with the look-ahead gather only for lanes on the trie (off it, no later step takes)
-    "lamask": [("sparc_kernels.hip", "if (lds_s && blocks <= 64) launch_s(k_rollout1s<TB, false, true, true, IOR>, d_act);",
-                "if (lds_s) launch_s(k_rollout1s<TB, false, true, true, IOR>, d_act);"),
-               ("sparc_trie.hpp", """        const uint2 rec = trieg[((base + (S & 0x7FFFu)) << 2) + (an & 3u)];
-        nrx = rec.x;
-        nry = rec.y;""", """        if (S < 0x10000u) {
-            const uint2 rec = trieg[((base + (S & 0x7FFFu)) << 2) + (an & 3u)];
-            nrx = rec.x;
-            nry = rec.y;
-        }""")],
-    # only the masked gather (c2's look-ahead grids)
-    "lamask2": [("sparc_trie.hpp", """        const uint2 rec = trieg[((base + (S & 0x7FFFu)) << 2) + (an & 3u)];
-        nrx = rec.x;
-        nry = rec.y;""", """        if (S < 0x10000u) {
-            const uint2 rec = trieg[((base + (S & 0x7FFFu)) << 2) + (an & 3u)];
-            nrx = rec.x;
-            nry = rec.y;
-        }""")],
     # k_rollout_obsw occupancy: waves per SIMD allowed by the register budget
     "obsw6": [("sparc_kernels.hip", "__launch_bounds__(kBlockOw) __attribute__((amdgpu_waves_per_eu(4)))",
                "__launch_bounds__(kBlockOw) __attribute__((amdgpu_waves_per_eu(6)))")],
