@@ -85,6 +85,9 @@ VARIANTS = {
     # k_rollout1s: the move and trie waves read a whole 16-step tile's inputs at once
     "group16": [("sparc_kernels.hip", "constexpr int kGroup1s = 4;", "constexpr int kGroup1s = 16;")],
     "group8": [("sparc_kernels.hip", "constexpr int kGroup1s = 4;", "constexpr int kGroup1s = 8;")],
+    # c2 (grids of at most 64 workgroups) on the plain trie wave instead of the look-ahead form
+    "nola": [("sparc_kernels.hip", "if (lds_s && blocks <= 64) launch_s(k_rollout1s<TB, false, true, true, IOR>, d_act);",
+              "if (lds_s && blocks <= 0) launch_s(k_rollout1s<TB, false, true, true, IOR>, d_act);")],
     "noprio": [("sparc_kernels.hip", """        __builtin_amdgcn_s_setprio(1);
         TrieLane tl;""", """        TrieLane tl;""")],
     # k_rollout1r with s_memtime stamps (timing only: the stats buffer receives, per wave, role |
