@@ -62,6 +62,19 @@ VARIANTS = {
     # the look-ahead trie wave (step1la) on every LDS-table grid, not only on <= 64 workgroups
     "la": [("sparc_kernels.hip", "if (lds_s && blocks <= 64) launch_s(k_rollout1s<TB, false, true, true, IOR>, d_act);",
             "if (lds_s) launch_s(k_rollout1s<TB, false, true, true, IOR>, d_act);")],
+    # "la" with the look-ahead gather issued by on-trie lanes only (off-trie lanes cannot take on
+    # the next step): fewer L2 requests at 65,536 envs, one exec-masked branch per step
+    "lamask": [("sparc_kernels.hip", "if (lds_s && blocks <= 64) launch_s(k_rollout1s<TB, false, true, true, IOR>, d_act);",
+                "if (lds_s) launch_s(k_rollout1s<TB, false, true, true, IOR>, d_act);"),
+               ("sparc_trie.hpp", """        const uint2 rec = trieg[((base + (S & 0x7FFFu)) << 2) + __builtin_amdgcn_ubfe(an16, 4u, 2u)];
+        nrx = rec.x;
+        nry = rec.y;
+        return finish""", """        if (S < 0x10000u) {
+            const uint2 rec = trieg[((base + (S & 0x7FFFu)) << 2) + __builtin_amdgcn_ubfe(an16, 4u, 2u)];
+            nrx = rec.x;
+            nry = rec.y;
+        }
+        return finish""")],
     # k_rollout_obsw occupancy: waves per SIMD allowed by the register budget
     "obsw6": [("sparc_kernels.hip", "__launch_bounds__(kBlockOw) __attribute__((amdgpu_waves_per_eu(4)))",
                "__launch_bounds__(kBlockOw) __attribute__((amdgpu_waves_per_eu(6)))")],
