@@ -205,6 +205,38 @@ int sparc_rollout_rules_device(void *ctx, int32_t T, const uint8_t *d_actions, u
                                int8_t *d_reward, uint8_t *d_flags, int32_t *d_stats, uint16_t *d_rule_bits);
 
 int sparc_read_state(void *ctx, const sparc_state_host *out);
+
+/* ---- one env in one round trip: the drop-in SPaRC_Gym (a context of one env) -----------------
+ * Everything SPaRC_Gym.step() / reset() returns for env `env` of the context, written by the
+ * kernels straight into a pinned record and read back with ONE stream synchronisation: the step's
+ * reward code and flags, the new state, and (audit != 0, after sparc_load_rules) the rule audit of
+ * the new state with its region ids and fit mask (info['rule_status'], _validate_rules 941-950).
+ * An exact fit past the GPU's node cap (rare) is finished on the host before the call returns, so
+ * rule_bits never holds SPARC_RULE_SEARCH_EXHAUSTED (one more synchronisation, that call only).
+ * The audit covers every env of the context (k_rules): meant for contexts of one env. */
+typedef struct {
+    int8_t reward_code;     /* the step's reward * 100 (0 after reset / read), SPaRC_Gym.py:1201-1223 */
+    uint8_t flags;          /* bit0 terminated, bit1 truncated, bits2-5 legal actions of the new state */
+    uint8_t x, y;           /* _agent_location                                                       */
+    uint8_t path_len;       /* len(self.path)                                                        */
+    int8_t outcome;         /* outcome_reward (info['Rewards'], 1020)                                */
+    uint8_t pending;        /* the last step was done (next-step autoreset pending)                 */
+    uint8_t audited;        /* 1: rule_bits / fit / region below are the new state's audit         */
+    uint32_t step;          /* current_step                                                          */
+    uint32_t puzzle;        /* current_puzzle_index                                                  */
+    uint16_t rule_bits;     /* SPARC_RULE_*                                                          */
+    uint16_t reserved;
+    uint32_t host_fits;     /* exact fits of this audit the host finished (0 on nearly every call)  */
+    uint64_t fit;           /* bit r: region r passed the poly/ylop area check and exact fit        */
+    uint64_t visited[4];    /* obs['base']['visited'] bits x*pitch + y (the first `words` words)    */
+    uint8_t region[256];    /* region id per cell bit (64 * words entries), 0xFF elsewhere          */
+} sparc_env_record;
+/* step (SPaRC_Gym.py:1111-1238) of env `env` with `action` (outside 0..3: illegal, no move) */
+int sparc_env_step(void *ctx, int32_t env, int32_t action, int32_t audit, sparc_env_record *out);
+/* reset / _load_puzzle (1057-1108, 95-217) of env `env` onto puzzle `puzzle_index` */
+int sparc_env_reset(void *ctx, int32_t env, uint32_t puzzle_index, int32_t audit, sparc_env_record *out);
+/* the current state (and audit) of env `env`, no transition */
+int sparc_env_read(void *ctx, int32_t env, int32_t audit, sparc_env_record *out);
 /* device-to-device copy of one SoA state array (`which` as in sparc_state_ptr) into d_out,
  * ordered on the context's stream (e.g. the per-env puzzle index after autoresets). */
 int sparc_copy_state_device(void *ctx, int32_t which, void *d_out);

@@ -116,6 +116,62 @@ __global__ void __launch_bounds__(kBlock) k_step(Params p, const uint8_t* __rest
     flg[i] = (uint8_t)f;
 }
 
+// One env of the context in one round trip (sparc_env_step / _reset / _read: the drop-in
+// SPaRC_Gym, SPaRC_Gym.py:1057-1238): op 0 reads the state, 1 steps it with action `arg`, 2 resets
+// it onto puzzle `arg`; the new state goes straight into the caller's pinned record.  One lane.
+template <int W, bool TB>
+__global__ void __launch_bounds__(64) k_env_op(Params p, uint32_t i, int32_t op, uint32_t arg,
+                                               sparc_env_record* __restrict__ rec) {
+    if (threadIdx.x != 0 || i >= p.n) return;
+    const PuzzleSrc<W> src{p.tab.info, p.tab.root, p.tab.open, p.tab.init, p.tab.row1};
+    Env<W, TB> e;
+    int code = 0;
+    uint32_t f = 0;
+    if (op == 2) {
+        e.reset(p, src, arg);
+        f = e.legal << 2;
+    } else {
+        e.load(p, src, i);
+        if (op == 1) code = e.advance(p, src, arg, f);
+        else f = e.legal << 2;
+    }
+    if (op != 0) e.store(p, src, i);
+    const State& s = p.st;
+    const uint32_t ps = s.pos[i], ax = s.aux[i], oc = (ax >> 16) & 3u;
+    rec->reward_code = (int8_t)code;
+    rec->flags = (uint8_t)f;
+    rec->x = (uint8_t)(ps & 0xFFu);
+    rec->y = (uint8_t)((ps >> 8) & 0xFFu);
+    rec->path_len = (uint8_t)((ps >> 16) & 0xFFu);
+    rec->outcome = (int8_t)(oc == 1u ? 1 : (oc == 2u ? -1 : 0));
+    rec->pending = (uint8_t)((ax >> 18) & 1u);
+    rec->audited = 0;
+    rec->step = s.step[i];
+    rec->puzzle = s.pid[i];
+    rec->rule_bits = 0;
+    rec->host_fits = 0;
+    rec->fit = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) rec->visited[k] = k < W ? s.vis[(size_t)k * p.n + i] : 0ull;
+}
+
+// the rule audit of env i (k_rules' outputs for every env of the context) and the exact fits it
+// queued for the host, into the same record
+__global__ void __launch_bounds__(64) k_env_audit(uint32_t i, uint32_t W, const uint16_t* __restrict__ bits,
+                                                  const uint8_t* __restrict__ region, const uint64_t* __restrict__ fit,
+                                                  const unsigned long long* __restrict__ queued,
+                                                  sparc_env_record* __restrict__ rec) {
+    const uint32_t l = threadIdx.x, nb = 64u * W;
+    for (uint32_t b = l; b < 256u; b += 64u) rec->region[b] = b < nb ? region[(size_t)i * nb + b] : (uint8_t)0xFF;
+    if (l == 0) {
+        const unsigned long long q = *queued;
+        rec->rule_bits = bits[i];
+        rec->fit = fit[i];
+        rec->host_fits = q > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)q;
+        rec->audited = 1;
+    }
+}
+
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // streamed-once I/O: nontemporal so that actions / outputs do not evict the trie from L2
@@ -250,9 +306,13 @@ struct ObsStream {
     uint32_t vis[128 * W + 1];   // 64 envs x at most 64 W bits, + the last lane's shifted spill
     uint32_t ag[128 * W + 1];
 };
-// stream staging applies: the board bit of cell (x, y) is x * YD + y
+// stream staging applies: the board bit of cell (x, y) is x * YD + y, and a run of 64 envs fits the
+// stream (XD * YD <= 64 W bits per env; a pool padded past its largest lattice, x_dim > x_max, can
+// have more cells than board bits and takes the LUT path)
 template <int W>
-__host__ __device__ constexpr bool obs_stream_ok(uint32_t pitch, uint32_t YD) { return W > 1 && pitch == YD; }
+__host__ __device__ constexpr bool obs_stream_ok(uint32_t pitch, uint32_t XD, uint32_t YD) {
+    return W > 1 && pitch == YD && XD * YD <= 64u * W;
+}
 
 template <int W>
 __device__ __forceinline__ void obs_stage_stream(ObsStream<W>* os, uint32_t lane, bool has_env,
@@ -662,7 +722,7 @@ __global__ void __launch_bounds__(kBlockOw) __attribute__((amdgpu_waves_per_eu(4
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr size_t kBuf = obsw_buf_bytes<W>();   // buffer (t & 1) * 4 + k at smem + that * kBuf
     uint16_t* lut = reinterpret_cast<uint16_t*>(smem + 8 * kBuf);
-    const bool stream = obs_stream_ok<W>(p.pitch, ot.YD);   // block-uniform
+    const bool stream = obs_stream_ok<W>(p.pitch, ot.XD, ot.YD);   // block-uniform
     if (stream) {   // the bit streams start at 0 (the writers zero them after each read)
         for (uint32_t k = threadIdx.x; k < 8 * kBuf / 4; k += kBlockOw) reinterpret_cast<uint32_t*>(smem)[k] = 0u;
     } else {
@@ -1765,7 +1825,7 @@ __global__ void __launch_bounds__(kBlock) k_rules(Params p, RulesTab rt, uint16_
 template <int W>
 __global__ void __launch_bounds__(kBlock) k_region_table(Params p, RulesTab rt, const uint2* __restrict__ items,
                                                          uint32_t count, uint32_t* __restrict__ tab,
-                                                         uint32_t* __restrict__ exhausted) {
+                                                         unsigned long long* __restrict__ exhausted) {
     const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
     if (k >= count) return;
     const uint2 it = items[k];
@@ -1773,7 +1833,7 @@ __global__ void __launch_bounds__(kBlock) k_region_table(Params p, RulesTab rt, 
     tab[rt.reg_off[it.x] / 8u + it.y] = w;
     uint32_t ex = 0;
     for (uint32_t j = 0; j < 8; ++j) ex += ((w >> (4u * j + kRcPolyShift)) & 3u) == 3u ? 1u : 0u;
-    if (ex) atomicAdd(exhausted, ex);
+    if (ex) atomicAdd(exhausted, (unsigned long long)ex);
 }
 
 // sparc_rules_finish's corrections of one output entry: rule bits &= ~clear, fit |= fit_or (the
@@ -1796,7 +1856,8 @@ __global__ void __launch_bounds__(kBlock) k_rule_patch(const RulePatch* __restri
 // extent (entries: N, or T * N), and for a generic rule rollout its launch, so that a call whose
 // queue overflowed runs again on a larger queue from the state it started from (Ctx::snap).
 struct AuditCall {
-    int kind = 0;   // 0 none, 1 sparc_rules_device, 2 rule rollout (snapshot taken)
+    int kind = 0;   // 0 none, 1 sparc_rules_device, 2 rule rollout
+    bool snap = false;   // kind 2: the generic rule kernel ran it from a snapshot (re-runnable)
     uint64_t extent = 0;
     uint16_t* bits = nullptr;
     uint8_t* region = nullptr;
@@ -1865,11 +1926,19 @@ struct Ctx {
     std::vector<uint2> h_inst_fc, h_shape_range;
     size_t host_fit_puzzles = 0;    // puzzles flagged kHostFit by the last sparc_load_rules
     std::vector<int8_t> h_shape_off;
-    uint32_t* fq_count = nullptr;   // FitQueue of the audits (sparc_rules_finish)
+    unsigned long long* fq_count = nullptr;   // FitQueue of the audits (sparc_rules_finish)
     FitTodo* fq_items = nullptr;
-    uint32_t fq_cap = 0;            // its capacity (grown by sparc_rules_finish on overflow)
+    uint64_t fq_cap = 0;            // its capacity (grown by sparc_rules_finish on overflow)
     uint64_t fq_last = 0, fq_reruns = 0;   // searches the last finish ran; calls run again
-    uint32_t* h_count = nullptr;    // pinned host word the queue count is read into
+    uint64_t* h_count = nullptr;    // pinned host word the queue count is read into
+    // answers of the host's exact fits (sparc_rules.hpp HostFits), so that later audits look them
+    // up instead of queueing the same search again: host mirror + device copy
+    std::vector<uint4> h_hf;
+    uint4* d_hf = nullptr;
+    uint32_t hf_used = 0;
+    // the one-env record of sparc_env_step / _reset / _read (pinned, written by the kernels)
+    sparc_env_record* h_rec = nullptr;
+    sparc_env_record* d_rec = nullptr;
     AuditCall last_audit;           // the last queueing audit call (sparc_rules_finish)
     // the state a generic rule rollout started from (re-run on a queue overflow)
     void* snap = nullptr;
@@ -1989,7 +2058,8 @@ struct R1Shape {
     static constexpr int G = G_, A = A_, RT = RT_;
 };
 
-constexpr uint32_t kFitQueueCap = 1u << 16;   // exact fits past the node cap per audit call
+constexpr uint64_t kFitQueueCap = 1u << 16;   // exact fits past the node cap per audit call (grown)
+constexpr uint64_t kFitQueueMax = (uint64_t)1 << 28;   // 6 GB of FitTodo
 
 // the loaded rule table as the kernels take it; queue: push searches past the node cap to the
 // FitQueue (audits), or not (the region-code table build: the host scans the table instead)
@@ -2007,6 +2077,7 @@ RulesTab rules_tab(const Ctx* c, bool queue) {
     rt.reg_off = c->r_reg_off;
     rt.reg_tab = c->r_reg_tab;
     rt.fq = FitQueue{queue ? c->fq_count : nullptr, c->fq_items, c->fq_cap};
+    rt.hf = HostFits{c->d_hf, c->h_hf.empty() ? 0u : (uint32_t)c->h_hf.size() - 1u, c->d_hf ? c->hf_used : 0u};
     rt.rows = c->r_rows;
     return rt;
 }
@@ -2113,11 +2184,13 @@ int sparc_destroy(void* ctx) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->vis, c->dirs, c->pos, c->aux, c->step, c->pid, c->t_open, c->t_info, c->t_root, c->t_trie, c->t_init, c->t_row1,
                     c->t_trie8, c->t_trow, c->t_mrow, c->t_mroww, c->t_boardw, c->err, c->s_act, c->s_flags, c->s_mask, c->s_rew, c->s_pidx, c->r_planes, c->r_inst_fc,
-                    c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off, c->r_memo, c->s_bits, c->s_region, c->s_fit, c->r_reg_off, c->r_reg_tab, c->fq_count, c->fq_items, c->r_rows};
+                    c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off, c->r_memo, c->s_bits, c->s_region, c->s_fit, c->r_reg_off, c->r_reg_tab, c->fq_count, c->fq_items, c->r_rows,
+                    c->t_trieg, c->d_hf};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->snap) (void)hipFree(c->snap);
     if (c->h_count) (void)hipHostFree(c->h_count);
+    if (c->h_rec) (void)hipHostFree(c->h_rec);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
     return SPARC_OK;
@@ -2781,7 +2854,11 @@ int snapshot(Ctx* c, int32_t* d_stats, bool save) {
 int launch_rules(Ctx* c, const AuditCall& a) {
     if (a.kind == 2) {
         const RuleTrace rtr{rules_tab(c, true), a.bits, c->r_memo};
-        return rollout_impl(c, a.T, a.act, a.seed, a.t0, a.rew, a.flags, a.stats, nullptr, &rtr);
+        const bool generic = c->rules_generic;
+        if (a.snap) c->rules_generic = true;   // the kernel the call was recorded with
+        const int rc = rollout_impl(c, a.T, a.act, a.seed, a.t0, a.rew, a.flags, a.stats, nullptr, &rtr);
+        c->rules_generic = generic;
+        return rc;
     }
     const Params p = make_params(c);
     const RulesTab rt = rules_tab(c, true);
@@ -2828,7 +2905,7 @@ int sparc_rollout_rules_device(void* ctx, int32_t T, const uint8_t* d_act, uint6
     if (!c->rules) return fail(c, SPARC_E_STATE, "sparc_load_rules has not been called");
     if (!d_rule_bits) return fail(c, SPARC_E_INVALID, "null rule_bits");
     if (T < 0) return fail(c, SPARC_E_INVALID, "T must be >= 0");
-    HIPCHK(c, hipMemsetAsync(c->fq_count, 0, sizeof(uint32_t), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->fq_count, 0, sizeof(*c->fq_count), c->stream));
     AuditCall a;
     a.kind = 2;
     a.extent = (uint64_t)T * c->n;
@@ -2840,10 +2917,13 @@ int sparc_rollout_rules_device(void* ctx, int32_t T, const uint8_t* d_act, uint6
     a.rew = d_rew;
     a.flags = d_flags;
     a.stats = d_stats;
-    c->last_audit = a;
     // the generic rule kernel queues searches past the node cap: keep the state it starts from, so
-    // that sparc_rules_finish can run the call again on a larger queue (k_rollout1r never queues)
-    if (!r1r_rollout(c)) {
+    // that sparc_rules_finish can run the call again on a larger queue (k_rollout1r never queues).
+    // The call records which it was: finish re-runs exactly this kernel, whatever
+    // sparc_set_variant has selected since
+    a.snap = !r1r_rollout(c);
+    c->last_audit = a;
+    if (a.snap) {
         rc = snapshot(c, d_stats, true);
         if (rc) return rc;
     }
@@ -3021,12 +3101,15 @@ int sparc_load_rules(void* ctx, const sparc_rules_table* t) {
     c->h_shape_off.assign(t->shape_off, t->shape_off + 2 * (size_t)t->num_offsets);
     c->h_shape_off.resize(2 * no, 0);
     if (!c->fq_count) {
-        HIPCHK(c, hipMalloc(&c->fq_count, sizeof(uint32_t)));
+        HIPCHK(c, hipMalloc(&c->fq_count, sizeof(*c->fq_count)));
         HIPCHK(c, hipMalloc(&c->fq_items, sizeof(FitTodo) * kFitQueueCap));
         c->fq_cap = kFitQueueCap;
     }
-    HIPCHK(c, hipMemset(c->fq_count, 0, sizeof(uint32_t)));
+    HIPCHK(c, hipMemset(c->fq_count, 0, sizeof(*c->fq_count)));
     c->last_audit = AuditCall{};
+    // the host's answers name puzzles of the old table
+    c->hf_used = 0;
+    std::fill(c->h_hf.begin(), c->h_hf.end(), make_uint4(0u, 0u, 0u, 0u));
     // the memo's entries name puzzles of the old table: start empty (a zero key matches no region)
     if (!c->r_memo) HIPCHK(c, hipMalloc(&c->r_memo, sizeof(FitMemo<kMemo>) * (size_t)c->n));
     HIPCHK(c, hipMemset(c->r_memo, 0, sizeof(FitMemo<kMemo>) * (size_t)c->n));
@@ -3071,10 +3154,10 @@ int sparc_load_rules(void* ctx, const sparc_rules_table* t) {
         HIPCHK(c, hipStreamSynchronize(c->stream));
         HIPCHK(c, hipFree(d_items));
         if (rc) return rc;
-        uint32_t exhausted = 0;
-        HIPCHK(c, hipMemcpy(&exhausted, c->fq_count, sizeof(uint32_t), hipMemcpyDeviceToHost));
+        unsigned long long exhausted = 0;
+        HIPCHK(c, hipMemcpy(&exhausted, c->fq_count, sizeof(exhausted), hipMemcpyDeviceToHost));
         if (exhausted) {   // finish those searches on the host and rewrite their codes
-            HIPCHK(c, hipMemset(c->fq_count, 0, sizeof(uint32_t)));
+            HIPCHK(c, hipMemset(c->fq_count, 0, sizeof(*c->fq_count)));
             std::vector<uint32_t> tab(words);
             HIPCHK(c, hipMemcpy(tab.data(), c->r_reg_tab, sizeof(uint32_t) * words, hipMemcpyDeviceToHost));
             parallel_for(items.size(), [&](size_t k) {   // each word belongs to one item
@@ -3110,6 +3193,143 @@ int sparc_load_rules(void* ctx, const sparc_rules_table* t) {
     return SPARC_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// per-env audit outputs of the host-pointer / one-env calls (device scratch)
+int audit_scratch(Ctx* c) {
+    if (c->s_bits) return SPARC_OK;
+    const size_t n = c->n;
+    HIPCHK(c, hipMalloc(&c->s_bits, 2 * n));
+    HIPCHK(c, hipMalloc(&c->s_region, n * 64 * c->W));
+    HIPCHK(c, hipMalloc(&c->s_fit, 8 * n));
+    return SPARC_OK;
+}
+
+// the FitQueue count of the last audit call (one stream sync)
+int read_queue_count(Ctx* c, uint64_t& n) {
+    if (!c->h_count) HIPCHK(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_count), sizeof(uint64_t), hipHostMallocDefault));
+    HIPCHK(c, hipMemcpyAsync(c->h_count, c->fq_count, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    n = *c->h_count;
+    return SPARC_OK;
+}
+
+// one answer into the host mirror of HostFits (false: already there)
+bool hostfits_insert(std::vector<uint4>& t, uint32_t q, uint64_t rm, uint32_t fits) {
+    const uint32_t mask = (uint32_t)t.size() - 1u;
+    for (uint32_t s = hostfit_slot(q, rm, mask);; s = (s + 1u) & mask) {
+        uint4& e = t[s];
+        if (!(e.w & 2u)) {
+            e = make_uint4((uint32_t)rm, (uint32_t)(rm >> 32), q, fits | 2u);
+            return true;
+        }
+        if (e.x == (uint32_t)rm && e.y == (uint32_t)(rm >> 32) && e.z == q) return false;
+    }
+}
+
+// Keep the answers of one finish for later audits (sparc_rules.hpp HostFits): the table grows to
+// keep its load factor <= 1/2, up to kHostFitsMax slots (64 MB); past that new answers are not
+// kept (audits then queue those searches again; the results are the same).
+constexpr size_t kHostFitsMin = (size_t)1 << 12, kHostFitsMax = (size_t)1 << 22;
+int hostfits_add(Ctx* c, const std::vector<std::pair<uint32_t, uint64_t>>& keys, const std::vector<int8_t>& res) {
+    const size_t need = (size_t)c->hf_used + keys.size();
+    size_t cap = c->h_hf.size();
+    if (2 * need > cap && cap < kHostFitsMax) {
+        size_t ncap = std::max(cap, kHostFitsMin);
+        while (2 * need > ncap && ncap < kHostFitsMax) ncap *= 2;
+        std::vector<uint4> t(ncap, make_uint4(0u, 0u, 0u, 0u));
+        for (const uint4& e : c->h_hf)
+            if (e.w & 2u) hostfits_insert(t, e.z, (uint64_t)e.x | ((uint64_t)e.y << 32), e.w & 1u);
+        c->h_hf.swap(t);
+        if (c->d_hf) HIPCHK(c, hipFree(c->d_hf));
+        c->d_hf = nullptr;
+        HIPCHK(c, hipMalloc(&c->d_hf, sizeof(uint4) * ncap));
+    }
+    bool added = false;
+    for (size_t k = 0; k < keys.size() && 2 * ((size_t)c->hf_used + 1) <= c->h_hf.size(); ++k)
+        if (hostfits_insert(c->h_hf, keys[k].first, keys[k].second, res[k] == 1 ? 1u : 0u)) {
+            ++c->hf_used;
+            added = true;
+        }
+    if (added) HIPCHK(c, hipMemcpyAsync(c->d_hf, c->h_hf.data(), sizeof(uint4) * c->h_hf.size(), hipMemcpyHostToDevice, c->stream));
+    return SPARC_OK;
+}
+
+// sparc_rules_finish once the queue count of the last audit call is known (cnt entries pushed)
+int finish_queue(Ctx* c, uint64_t cnt, uint16_t* d_bits, uint64_t* d_fit) {
+    int rc = SPARC_OK;
+    c->fq_last = cnt;
+    if (cnt == 0) return SPARC_OK;
+    const AuditCall a = c->last_audit;
+    if (a.kind == 0) return fail(c, SPARC_E_STATE, "queued exact-fit searches without a recorded audit call");
+    if (!d_bits || d_bits != a.bits) return fail(c, SPARC_E_STATE, "sparc_rules_finish: not the last audit call's bits");
+    if (cnt > c->fq_cap) {
+        // the queue overflowed: a larger queue, and the call again from where it started (an
+        // audit is deterministic: the same searches are queued, and the memo holds final answers)
+        if (a.kind == 2 && !a.snap) return fail(c, SPARC_E_STATE, "queue overflow of a rule rollout without a snapshot");
+        uint64_t cap = c->fq_cap;
+        while (cap < cnt) cap *= 2;
+        if (cap > kFitQueueMax) return fail(c, SPARC_E_NOMEM, "exact-fit queue past 2^28 entries in one audit call");
+        HIPCHK(c, hipFree(c->fq_items));
+        c->fq_items = nullptr;
+        c->fq_cap = 0;
+        HIPCHK(c, hipMalloc(&c->fq_items, sizeof(FitTodo) * cap));
+        c->fq_cap = cap;
+        if (a.kind == 2 && (rc = snapshot(c, a.stats, false))) return rc;
+        HIPCHK(c, hipMemsetAsync(c->fq_count, 0, sizeof(*c->fq_count), c->stream));
+        if ((rc = launch_rules(c, a))) return rc;
+        ++c->fq_reruns;
+        if ((rc = read_queue_count(c, cnt))) return rc;
+        if (cnt > c->fq_cap) return fail(c, SPARC_E_STATE, "exact-fit queue overflow on the re-run");
+    }
+    std::vector<FitTodo> todo(cnt);
+    HIPCHK(c, hipMemcpy(todo.data(), c->fq_items, sizeof(FitTodo) * cnt, hipMemcpyDeviceToHost));
+    c->fq_last = cnt;
+    for (const FitTodo& it : todo)
+        if (it.pos >= a.extent || it.q >= c->num_puzzles)
+            return fail(c, SPARC_E_STATE, "exact-fit queue entry outside the last audit call");
+    // each distinct (puzzle, region cells) search once, on up to 16 host threads
+    std::vector<std::pair<uint32_t, uint64_t>> keys(cnt);
+    for (uint64_t k = 0; k < cnt; ++k) keys[k] = {todo[k].q, todo[k].rm};
+    std::sort(keys.begin(), keys.end());
+    keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+    std::vector<int8_t> res(keys.size(), 0);
+    parallel_for(keys.size(), [&](size_t k) { res[k] = (int8_t)host_fit(c, keys[k].first, keys[k].second); });
+    auto fits = [&](uint32_t q, uint64_t rm) {
+        const auto it = std::lower_bound(keys.begin(), keys.end(), std::make_pair(q, rm));
+        return res[(size_t)(it - keys.begin())] == 1;
+    };
+    // per output entry: every queued region's answer (all must fit for poly_ylop_area), and the
+    // fit mask of the regions that do
+    std::sort(todo.begin(), todo.end(), [](const FitTodo& x, const FitTodo& y) { return x.pos < y.pos; });
+    std::vector<RulePatch> patch;
+    for (size_t k = 0; k < todo.size();) {
+        RulePatch r{todo[k].pos, 0ull, SPARC_RULE_SEARCH_EXHAUSTED, 0u};
+        bool ok = true;
+        for (; k < todo.size() && todo[k].pos == r.pos; ++k) {
+            const bool f = fits(todo[k].q, todo[k].rm);
+            ok &= f;
+            if (f) r.fit_or |= 1ull << (todo[k].rid & 63u);
+        }
+        if (!ok) r.clear |= SPARC_RULE_POLY_YLOP | SPARC_RULE_ALL;
+        patch.push_back(r);
+    }
+    RulePatch* d_patch = nullptr;
+    HIPCHK(c, hipMalloc(&d_patch, sizeof(RulePatch) * patch.size()));
+    HIPCHK(c, hipMemcpyAsync(d_patch, patch.data(), sizeof(RulePatch) * patch.size(), hipMemcpyHostToDevice, c->stream));
+    k_rule_patch<<<grid_for(patch.size()), kBlock, 0, c->stream>>>(d_patch, (uint32_t)patch.size(), d_bits, d_fit);
+    rc = launch_check(c);
+    HIPCHK(c, hipMemsetAsync(c->fq_count, 0, sizeof(*c->fq_count), c->stream));
+    if (!rc) rc = hostfits_add(c, keys, res);
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipFree(d_patch));
+    return rc;
+}
+}  // namespace
+
+extern "C" {
+
 int sparc_rules_device(void* ctx, uint16_t* d_bits, uint8_t* d_region, uint64_t* d_fit) {
     DevGuard dg;
     Ctx* c = static_cast<Ctx*>(ctx);
@@ -3118,7 +3338,7 @@ int sparc_rules_device(void* ctx, uint16_t* d_bits, uint8_t* d_region, uint64_t*
     if (!c->rules) return fail(c, SPARC_E_STATE, "sparc_load_rules has not been called");
     // a fresh queue for this call (a caller that skipped sparc_rules_finish leaves no entries that
     // name another call's outputs), and the call recorded for sparc_rules_finish
-    HIPCHK(c, hipMemsetAsync(c->fq_count, 0, sizeof(uint32_t), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->fq_count, 0, sizeof(*c->fq_count), c->stream));
     AuditCall a;
     a.kind = 1;
     a.extent = c->n;
@@ -3179,78 +3399,9 @@ int sparc_rules_finish(void* ctx, uint16_t* d_bits, uint64_t* d_fit) {
     int rc = check_ctx(c, false);
     if (rc) return rc;
     if (!c->rules) return fail(c, SPARC_E_STATE, "sparc_load_rules has not been called");
-    if (!c->h_count) HIPCHK(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_count), sizeof(uint32_t), hipHostMallocDefault));
-    auto read_count = [&](uint32_t& n) -> int {
-        HIPCHK(c, hipMemcpyAsync(c->h_count, c->fq_count, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        n = *c->h_count;
-        return SPARC_OK;
-    };
-    uint32_t cnt = 0;
-    if ((rc = read_count(cnt))) return rc;
-    if (cnt == 0) return SPARC_OK;
-    const AuditCall a = c->last_audit;
-    if (a.kind == 0) return fail(c, SPARC_E_STATE, "queued exact-fit searches without a recorded audit call");
-    if (!d_bits || d_bits != a.bits) return fail(c, SPARC_E_STATE, "sparc_rules_finish: not the last audit call's bits");
-    if (cnt > c->fq_cap) {
-        // the queue overflowed: a larger queue, and the call again from where it started (an
-        // audit is deterministic: the same searches are queued, and the memo holds final answers)
-        if (a.kind == 2 && r1r_rollout(c)) return fail(c, SPARC_E_STATE, "queue overflow of a rule rollout without a snapshot");
-        uint64_t cap = c->fq_cap;
-        while (cap < cnt) cap *= 2;
-        HIPCHK(c, hipFree(c->fq_items));
-        c->fq_items = nullptr;
-        c->fq_cap = 0;
-        HIPCHK(c, hipMalloc(&c->fq_items, sizeof(FitTodo) * cap));
-        c->fq_cap = (uint32_t)std::min<uint64_t>(cap, 0xFFFFFFFFull);
-        if (a.kind == 2 && (rc = snapshot(c, a.stats, false))) return rc;
-        HIPCHK(c, hipMemsetAsync(c->fq_count, 0, sizeof(uint32_t), c->stream));
-        if ((rc = launch_rules(c, a))) return rc;
-        ++c->fq_reruns;
-        if ((rc = read_count(cnt))) return rc;
-        if (cnt > c->fq_cap) return fail(c, SPARC_E_STATE, "exact-fit queue overflow on the re-run");
-    }
-    std::vector<FitTodo> todo(cnt);
-    HIPCHK(c, hipMemcpy(todo.data(), c->fq_items, sizeof(FitTodo) * cnt, hipMemcpyDeviceToHost));
-    c->fq_last = cnt;
-    for (const FitTodo& it : todo)
-        if (it.pos >= a.extent || it.q >= c->num_puzzles)
-            return fail(c, SPARC_E_STATE, "exact-fit queue entry outside the last audit call");
-    // each distinct (puzzle, region cells) search once, on up to 16 host threads
-    std::vector<std::pair<uint32_t, uint64_t>> keys(cnt);
-    for (uint32_t k = 0; k < cnt; ++k) keys[k] = {todo[k].q, todo[k].rm};
-    std::sort(keys.begin(), keys.end());
-    keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
-    std::vector<int8_t> res(keys.size(), 0);
-    parallel_for(keys.size(), [&](size_t k) { res[k] = (int8_t)host_fit(c, keys[k].first, keys[k].second); });
-    auto fits = [&](uint32_t q, uint64_t rm) {
-        const auto it = std::lower_bound(keys.begin(), keys.end(), std::make_pair(q, rm));
-        return res[(size_t)(it - keys.begin())] == 1;
-    };
-    // per output entry: every queued region's answer (all must fit for poly_ylop_area), and the
-    // fit mask of the regions that do
-    std::sort(todo.begin(), todo.end(), [](const FitTodo& x, const FitTodo& y) { return x.pos < y.pos; });
-    std::vector<RulePatch> patch;
-    for (size_t k = 0; k < todo.size();) {
-        RulePatch r{todo[k].pos, 0ull, SPARC_RULE_SEARCH_EXHAUSTED, 0u};
-        bool ok = true;
-        for (; k < todo.size() && todo[k].pos == r.pos; ++k) {
-            const bool f = fits(todo[k].q, todo[k].rm);
-            ok &= f;
-            if (f) r.fit_or |= 1ull << (todo[k].rid & 63u);
-        }
-        if (!ok) r.clear |= SPARC_RULE_POLY_YLOP | SPARC_RULE_ALL;
-        patch.push_back(r);
-    }
-    RulePatch* d_patch = nullptr;
-    HIPCHK(c, hipMalloc(&d_patch, sizeof(RulePatch) * patch.size()));
-    HIPCHK(c, hipMemcpyAsync(d_patch, patch.data(), sizeof(RulePatch) * patch.size(), hipMemcpyHostToDevice, c->stream));
-    k_rule_patch<<<grid_for(patch.size()), kBlock, 0, c->stream>>>(d_patch, (uint32_t)patch.size(), d_bits, d_fit);
-    rc = launch_check(c);
-    HIPCHK(c, hipMemsetAsync(c->fq_count, 0, sizeof(uint32_t), c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    HIPCHK(c, hipFree(d_patch));
-    return rc;
+    uint64_t cnt = 0;
+    if ((rc = read_queue_count(c, cnt))) return rc;
+    return finish_queue(c, cnt, d_bits, d_fit);
 }
 
 int sparc_rules_host(void* ctx, uint16_t* bits, uint8_t* region, uint64_t* fit) {
@@ -3259,19 +3410,87 @@ int sparc_rules_host(void* ctx, uint16_t* bits, uint8_t* region, uint64_t* fit) 
     int rc = check_ctx(c, true);
     if (rc) return rc;
     const size_t n = c->n, rb = n * 64 * c->W;
-    if (!c->s_bits) {
-        HIPCHK(c, hipMalloc(&c->s_bits, 2 * n));
-        HIPCHK(c, hipMalloc(&c->s_region, rb));
-        HIPCHK(c, hipMalloc(&c->s_fit, 8 * n));
-    }
+    if ((rc = audit_scratch(c))) return rc;
     rc = sparc_rules_device(c, c->s_bits, region ? c->s_region : nullptr, fit ? c->s_fit : nullptr);
     if (rc) return rc;
-    rc = sparc_rules_finish(c, c->s_bits, fit ? c->s_fit : nullptr);
-    if (rc) return rc;
+    // the queue count travels with the outputs: one synchronisation when nothing was queued (an
+    // exact fit past the GPU's node cap is rare), else the host finishes the searches and the
+    // patched bits / fit are read again
+    if (!c->h_count) HIPCHK(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_count), sizeof(uint64_t), hipHostMallocDefault));
+    HIPCHK(c, hipMemcpyAsync(c->h_count, c->fq_count, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
     if (bits) HIPCHK(c, hipMemcpyAsync(bits, c->s_bits, 2 * n, hipMemcpyDeviceToHost, c->stream));
     if (region) HIPCHK(c, hipMemcpyAsync(region, c->s_region, rb, hipMemcpyDeviceToHost, c->stream));
     if (fit) HIPCHK(c, hipMemcpyAsync(fit, c->s_fit, 8 * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const uint64_t cnt = *c->h_count;
+    if ((rc = finish_queue(c, cnt, c->s_bits, fit ? c->s_fit : nullptr)) || cnt == 0) return rc;
+    if (bits) HIPCHK(c, hipMemcpyAsync(bits, c->s_bits, 2 * n, hipMemcpyDeviceToHost, c->stream));
+    if (fit) HIPCHK(c, hipMemcpyAsync(fit, c->s_fit, 8 * n, hipMemcpyDeviceToHost, c->stream));
     return sparc_sync(c);
+}
+
+}  // extern "C"
+
+namespace {
+// one env, one round trip (sparc_env_step / _reset / _read)
+int env_call(Ctx* c, int32_t env, int32_t op, uint32_t arg, int32_t audit, sparc_env_record* out) {
+    int rc = check_ctx(c, op != 2);
+    if (rc) return rc;
+    if (!out) return fail(c, SPARC_E_INVALID, "null record");
+    if (env < 0 || (uint32_t)env >= c->n) return fail(c, SPARC_E_INVALID, "env index out of range");
+    if (op == 2 && !c->has_state && c->n != 1)
+        return fail(c, SPARC_E_STATE, "first reset must cover every env (sparc_reset_*)");
+    if (op == 2 && arg >= c->num_puzzles) return fail(c, SPARC_E_INVALID, "puzzle index out of range");
+    if (audit && !c->rules) return fail(c, SPARC_E_STATE, "sparc_load_rules has not been called");
+    if (!c->h_rec) {
+        HIPCHK(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_rec), sizeof(sparc_env_record), hipHostMallocMapped));
+        HIPCHK(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_rec), c->h_rec, 0));
+    }
+    const Params p = make_params(c);
+    dispatch_w_tb(c->W, c->cfg.traceback, [&](auto w, auto tb) {
+        k_env_op<decltype(w)::value, decltype(tb)::value><<<1, 64, 0, c->stream>>>(p, (uint32_t)env, op, arg, c->d_rec);
+    });
+    if ((rc = launch_check(c))) return rc;
+    if (op == 2) c->has_state = true;
+    if (audit) {
+        if ((rc = audit_scratch(c))) return rc;
+        if ((rc = sparc_rules_device(c, c->s_bits, c->s_region, c->s_fit))) return rc;
+        k_env_audit<<<1, 64, 0, c->stream>>>((uint32_t)env, (uint32_t)c->W, c->s_bits, c->s_region, c->s_fit,
+                                             c->fq_count, c->d_rec);
+        if ((rc = launch_check(c))) return rc;
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    *out = *c->h_rec;
+    if (audit) c->fq_last = 0;
+    if (audit && out->host_fits) {   // exact fits past the GPU's node cap: finished on the host
+        uint64_t cnt = 0;
+        if ((rc = read_queue_count(c, cnt))) return rc;
+        if ((rc = finish_queue(c, cnt, c->s_bits, c->s_fit))) return rc;
+        HIPCHK(c, hipMemcpyAsync(&out->rule_bits, c->s_bits + env, 2, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(&out->fit, c->s_fit + env, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    return SPARC_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int sparc_env_step(void* ctx, int32_t env, int32_t action, int32_t audit, sparc_env_record* out) {
+    DevGuard dg;
+    // outside 0..3 nothing is legal (`action in legal_actions` fails, SPaRC_Gym.py:1137)
+    const uint32_t a = (action >= 0 && action < 4) ? (uint32_t)action : 255u;
+    return env_call(static_cast<Ctx*>(ctx), env, 1, a, audit, out);
+}
+
+int sparc_env_reset(void* ctx, int32_t env, uint32_t puzzle_index, int32_t audit, sparc_env_record* out) {
+    DevGuard dg;
+    return env_call(static_cast<Ctx*>(ctx), env, 2, puzzle_index, audit, out);
+}
+
+int sparc_env_read(void* ctx, int32_t env, int32_t audit, sparc_env_record* out) {
+    DevGuard dg;
+    return env_call(static_cast<Ctx*>(ctx), env, 0, 0u, audit, out);
 }
 
 int sparc_read_state(void* ctx, const sparc_state_host* o) {

@@ -71,13 +71,38 @@ struct FitTodo {
     uint32_t q, rid;
 };
 struct FitQueue {
-    uint32_t* count;   // entries pushed (may pass cap: the host then reports the overflow)
+    unsigned long long* count;   // entries pushed (may pass cap: the host grows the queue and re-runs)
     FitTodo* items;
-    uint32_t cap;
+    uint64_t cap;
 };
 __device__ __forceinline__ void fit_queue_push(const FitQueue& fq, uint64_t pos, uint64_t rm, uint32_t q, uint32_t rid) {
-    const uint32_t k = atomicAdd(fq.count, 1u);
+    const unsigned long long k = atomicAdd(fq.count, 1ull);   // 64-bit: no wrap however many are queued
     if (k < fq.cap) fq.items[k] = FitTodo{pos, rm, q, rid};
+}
+
+// Exact-fit answers the host has finished (sparc_rules_finish: searches past the node cap, and
+// every search of a kHostFit puzzle), kept on the device so that an audit looks them up instead of
+// queueing the same (puzzle, region cells) search again at every later step.  Open addressing over
+// (q, rm), linear probing, load factor <= 1/2 (so a probe always ends at an empty slot); entry
+// {rm low, rm high, q, answer | valid << 1}.  used == 0: empty (no probe at all).
+struct HostFits {
+    const uint4* tab;
+    uint32_t mask;   // slots - 1 (a power of two)
+    uint32_t used;
+};
+__host__ __device__ __forceinline__ uint32_t hostfit_slot(uint32_t q, uint64_t rm, uint32_t mask) {
+    uint64_t h = rm * 0x9E3779B97F4A7C15ull ^ ((uint64_t)q * 0xC2B2AE3D27D4EB4Full);
+    h ^= h >> 29;
+    return (uint32_t)h & mask;
+}
+// 1 / 0: the host's answer, -1: not finished on the host
+__device__ __forceinline__ int hostfit_find(const HostFits& hf, uint32_t q, uint64_t rm) {
+    if (hf.used == 0) return -1;
+    for (uint32_t s = hostfit_slot(q, rm, hf.mask);; s = (s + 1u) & hf.mask) {
+        const uint4 e = hf.tab[s];
+        if (!(e.w & 2u)) return -1;
+        if (e.x == (uint32_t)rm && e.y == (uint32_t)(rm >> 32) && e.z == q) return (int)(e.w & 1u);
+    }
 }
 
 struct RulesTab {
@@ -97,6 +122,7 @@ struct RulesTab {
     const uint32_t* __restrict__ reg_off;
     const uint32_t* __restrict__ reg_tab;
     FitQueue fq;   // count null: no queue (region-table builds: the host scans the table instead)
+    HostFits hf;   // answers the host finished for earlier audits (looked up before a GPU search)
     // [P][rule_row_u64<W>()]: what an audit reads when its env changes puzzle, in one contiguous
     // record (puzzle_rules): the kBasePlanes planes, then reg_off | inst first << 32, then the
     // puzzle's info words x | y << 32 with y's bits 24-31 = instance count | host-fit flag << 7
@@ -456,7 +482,8 @@ __device__ uint32_t region_code(const RulesTab& rt, const FitIn& fin, uint32_t q
             int r = -1;
             if constexpr (!std::is_same<Memo, NoMemo>::value) r = memo->find(q, rm);
             if (r < 0) {
-                r = exact_fit<W>(fin, Rc, rm, fin.cap);
+                r = hostfit_find(rt.hf, q, rm);                  // finished on the host earlier
+                if (r < 0) r = exact_fit<W>(fin, Rc, rm, fin.cap);
                 if constexpr (!std::is_same<Memo, NoMemo>::value)
                     if (r >= 0) memo->put(q, rm, r);
             }

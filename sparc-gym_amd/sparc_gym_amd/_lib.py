@@ -39,6 +39,19 @@ class SparcRulesTable(ctypes.Structure):
                 ("shape_first", c_void_p), ("shape_area", c_void_p), ("shape_off", c_void_p)]
 
 
+class SparcEnvRecord(ctypes.Structure):
+    """sparc_env_record: one env after sparc_env_step / _reset / _read (one round trip)."""
+    _fields_ = [("reward_code", ctypes.c_int8), ("flags", ctypes.c_uint8), ("x", ctypes.c_uint8),
+                ("y", ctypes.c_uint8), ("path_len", ctypes.c_uint8), ("outcome", ctypes.c_int8),
+                ("pending", ctypes.c_uint8), ("audited", ctypes.c_uint8), ("step", ctypes.c_uint32),
+                ("puzzle", ctypes.c_uint32), ("rule_bits", ctypes.c_uint16), ("reserved", ctypes.c_uint16),
+                ("host_fits", ctypes.c_uint32), ("fit", ctypes.c_uint64), ("visited", ctypes.c_uint64 * 4),
+                ("region", ctypes.c_uint8 * 256)]
+
+
+assert ctypes.sizeof(SparcEnvRecord) == 320
+
+
 _SIGS = {
     "sparc_abi_version": ([], c_int32),
     "sparc_last_error": ([c_void_p], ctypes.c_char_p),
@@ -66,6 +79,9 @@ _SIGS = {
     "sparc_rollout_rules_device": ([c_void_p, c_int32, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p,
                                     c_void_p], c_int32),
     "sparc_read_state": ([c_void_p, ctypes.POINTER(SparcStateHost)], c_int32),
+    "sparc_env_step": ([c_void_p, c_int32, c_int32, c_int32, ctypes.POINTER(SparcEnvRecord)], c_int32),
+    "sparc_env_reset": ([c_void_p, c_int32, ctypes.c_uint32, c_int32, ctypes.POINTER(SparcEnvRecord)], c_int32),
+    "sparc_env_read": ([c_void_p, c_int32, c_int32, ctypes.POINTER(SparcEnvRecord)], c_int32),
     "sparc_state_ptr": ([c_void_p, c_int32, ctypes.POINTER(c_void_p)], c_int32),
     "sparc_set_visited_host": ([c_void_p, c_void_p], c_int32),
     "sparc_copy_state_device": ([c_void_p, c_int32, c_void_p], c_int32),

@@ -159,6 +159,30 @@ class SparcCore:
         self._check(self.lib.sparc_read_state(self.ctx, ctypes.byref(s)))
         return out
 
+    # ---------------------------------------------------------------- one env, one round trip
+    def env_step(self, action, audit=False, env=0):
+        """sparc_env_step: step env `env` and return its record (state, reward code, flags and,
+        with ``audit``, the rule audit of the new state) after ONE stream synchronisation."""
+        rec = self._rec()
+        self._check(self.lib.sparc_env_step(self.ctx, int(env), int(action), int(bool(audit)), ctypes.byref(rec)))
+        return rec
+
+    def env_reset(self, puzzle_index, audit=False, env=0):
+        rec = self._rec()
+        self._check(self.lib.sparc_env_reset(self.ctx, int(env), int(puzzle_index), int(bool(audit)),
+                                             ctypes.byref(rec)))
+        self.has_state = True
+        return rec
+
+    def env_read(self, audit=False, env=0):
+        rec = self._rec()
+        self._check(self.lib.sparc_env_read(self.ctx, int(env), int(bool(audit)), ctypes.byref(rec)))
+        return rec
+
+    def _rec(self):
+        # a fresh record per call: a caller may keep the previous one
+        return _lib.SparcEnvRecord()
+
     def set_visited_host(self, words):
         """Overwrite the visited boards [words][N] uint64 of the current state."""
         v = np.ascontiguousarray(words, np.uint64)

@@ -137,6 +137,8 @@ class SPaRC_Gym(Env):
         if self._audit:
             self._core.load_rules(pack_rules(self.puzzles, self._core.table))
         self._legal = 0
+        self._rec = None          # the last one-env record (sparc_env_*), its audit for _validate_rules
+        self._bit_index = {}      # (x_size, y_size) -> visited-board word / bit of every plane cell
         self._load_puzzle(self.current_puzzle_index)
         self._validate_rules()                                                       # 182
 
@@ -166,9 +168,10 @@ class SPaRC_Gym(Env):
         self._agent_location = np.array([self.start_location[0], self.start_location[1]], dtype=np.int32)
         self._target_location = np.array([self.target_location[0], self.target_location[1]], dtype=np.int32)
 
-        flags = self._core.reset_host(np.array([index], np.uint32))
-        self._legal = int(flags[0] >> 2) & 0xF
         if self.alias_compat:
+            self._rec = None
+            flags = self._core.reset_host(np.array([index], np.uint32))
+            self._legal = int(flags[0] >> 2) & 0xF
             sx, sy = int(self.start_location[0]), int(self.start_location[1])
             vis = self.obs_array["visited"]
             vis[sx, sy] = 1                                                          # 185
@@ -179,7 +182,10 @@ class SPaRC_Gym(Env):
             self.current_step = int(st["step"][0])
             self.outcome_reward = int(st["outcome"][0])
         else:
-            self._sync_planes()
+            # reset, the new state and its rule audit in one round trip (sparc_env_reset)
+            rec = self._core.env_reset(index, audit=self._audit)
+            self._apply_record(rec)
+            self._legal = (rec.flags >> 2) & 0xF
         self.obs_array["target_location"][self._target_location[0], self._target_location[1]] = 1
 
         if self.observation == "new":                                                # 190-196
@@ -199,6 +205,26 @@ class SPaRC_Gym(Env):
         self.action_space = Discrete(4)                                              # 210
         self._action_to_direction = {0: np.array([1, 0]), 1: np.array([0, -1]),
                                      2: np.array([-1, 0]), 3: np.array([0, 1])}
+
+    def _apply_record(self, rec):
+        """The device state of a one-env record -> visited / agent_location planes, step, outcome
+        (fresh planes: the agent plane holds the agent alone).  Keeps the record for the audit."""
+        X, Y = self.x_size, self.y_size
+        idx = self._bit_index.get((X, Y))
+        if idx is None:
+            pitch = self._core.table.pitch
+            xs, ys = np.meshgrid(np.arange(X), np.arange(Y), indexing="ij")
+            b = (xs * pitch + ys).astype(np.uint64)
+            idx = self._bit_index[(X, Y)] = ((b >> np.uint64(6)).astype(np.int64), b & np.uint64(63))
+        words = np.frombuffer(rec.visited, dtype=np.uint64)
+        self.obs_array["visited"][...] = ((words[idx[0]] >> idx[1]) & np.uint64(1)).astype(np.int32)
+        agent = self.obs_array["agent_location"]
+        agent[...] = 0
+        agent[rec.x, rec.y] = 1
+        self.current_step = int(rec.step)
+        self.outcome_reward = int(rec.outcome)
+        self._rec = rec
+        return rec.x, rec.y, rec.path_len
 
     def _sync_planes(self, old=None):
         """Mirror visited / agent_location planes from the device state.  alias_compat: the
@@ -262,10 +288,18 @@ class SPaRC_Gym(Env):
         return self._get_obs(), self._get_info()
 
     def step(self, action):
-        """SPaRC_Gym.py:1111-1238; the transition runs in the HIP step kernel."""
-        codes, flags = self._core.step_host(np.array([action_code(action)], np.uint8))
+        """SPaRC_Gym.py:1111-1238; the transition runs in the HIP step kernel.  Without
+        alias_compat the step, the new state and the rule audit of _get_info come back in ONE
+        round trip (sparc_env_step: one stream synchronisation)."""
         old = (int(self._agent_location[0]), int(self._agent_location[1]))
-        x, y, plen = self._sync_planes(old)
+        if self.alias_compat:
+            codes, flags = self._core.step_host(np.array([action_code(action)], np.uint8))
+            x, y, plen = self._sync_planes(old)
+            code, f = int(codes[0]), int(flags[0])
+        else:
+            rec = self._core.env_step(action_code(action), audit=self._audit)
+            x, y, plen = self._apply_record(rec)
+            code, f = int(rec.reward_code), int(rec.flags)
         if (x, y) != old:
             if plen < len(self.path):                                                # traceback pop
                 if self.observation == "SPaRC":
@@ -278,10 +312,9 @@ class SPaRC_Gym(Env):
             if self.observation == "SPaRC":
                 self.observ[y][x] = "L"
             self._agent_location = np.array([x, y], dtype=np.int64)
-        f = int(flags[0])
         terminated, truncated = bool(f & 1), bool(f & 2)
         self._legal = (f >> 2) & 0xF
-        self.normal_reward = reward_value(codes[0])
+        self.normal_reward = reward_value(code)
         return self._get_obs(), self.normal_reward, terminated, truncated, self._get_info()
 
     def _get_obs(self):
@@ -299,7 +332,15 @@ class SPaRC_Gym(Env):
         if not self._audit:
             self.rule_status = {}
             return self.rule_status
-        r = self._core.rules_host(region=True, fit=True)
+        if not self.alias_compat:
+            # the audit of the current state: from the last step / reset record, else one read
+            rec = self._rec if self._rec is not None and self._rec.audited else self._core.env_read(audit=True)
+            self._rec = rec
+            W = self._core.table.words
+            r = {"bits": [rec.rule_bits], "region": [np.frombuffer(rec.region, np.uint8)[:64 * W]],
+                 "fit": [rec.fit]}
+        else:
+            r = self._core.rules_host(region=True, fit=True)
         if self.alias_compat:
             # the path-based rules and the regions read self.path (400, 503-515, 639), the dots
             # rule the visited plane (529): with stale plane bits the audit runs on the path's

@@ -67,18 +67,20 @@ def _sharded_oracle(proc, pids, acts_list, tb, ms, shards=16):
     return outs, np.concatenate(stats), {k: np.concatenate([s[k] for s in states]) for k in states[0]}
 
 
-def test_c3_full_size_4096_puzzle_pool_vs_oracle(on_gpu):
+@pytest.mark.parametrize("P", [4096, 16384])
+def test_c3_full_size_big_puzzle_pool_vs_oracle(on_gpu, P):
     """c3 (65,536 envs, 7x7 full property set, traceback, max_steps 2,000, next-step autoreset)
-    on a 4,096-puzzle pool (bench.make_pool: the bench's 1,024-puzzle pool and three more
-    blocks), env i -> puzzle i * 2654435761 mod 4,096, actions drawn as the bench's, two
-    back-to-back 2,000-step launches through the bench's C-ABI call: every env bit-exact against
-    the C oracle (SPaRC_Gym.py:1111-1238, reset 1087)."""
+    on a 4,096- and a 16,384-puzzle pool (bench.make_pool: the bench's 1,024-puzzle pool and more
+    blocks; 16,384 is the pool of the bench line whose trie records outgrow an XCD's L2), env i ->
+    puzzle i * 2654435761 mod P, actions drawn as the bench's, two back-to-back 2,000-step
+    launches through the bench's C-ABI call: every env bit-exact against the C oracle
+    (SPaRC_Gym.py:1111-1238, reset 1087)."""
     import bench
     from sparc_gym_amd import SPaRCVecEnv
     os.environ["SPARC_POOL_WORKERS"] = "1"   # no worker processes from a process that drives the GPU
-    proc = bench.make_pool(4096, ((3, 3),), True)
+    proc = bench.make_pool(P, ((3, 3),), True)
     table = pack_table(proc)
-    assert len(proc) == 4096 > LDS_ROW_LIMIT and table.words == 1
+    assert len(proc) == P > LDS_ROW_LIMIT and table.words == 1
     n, T, L = 65536, 2000, 2
     pids = (np.arange(n, dtype=np.uint64) * 2654435761 % len(proc)).astype(np.int64)
     v = SPaRCVecEnv(n, processed=proc, table=table, traceback=True, max_steps=2000, autoreset="next_step",
@@ -104,7 +106,7 @@ def test_c3_full_size_4096_puzzle_pool_vs_oracle(on_gpu):
     assert np.array_equal(stats.cpu().numpy(), ost)
     _state_equal(v.state(), so, table)
     # the pool's far end is reached and episodes end both ways, with autoresets after them
-    assert int(so["pid"].max()) >= 3 * 1024
+    assert int(so["pid"].max()) >= 3 * P // 4
     f_all = f_np.reshape(-1, n)
     assert ((f_all & 1) != 0).sum() > 0 and ((f_all & 2) != 0).sum() > 0 and ((f_all & 64) != 0).sum() > 0
 

@@ -14,6 +14,14 @@
 * c4c: the same 262,144-env mixed pool without planes, through the multi-word split kernel
   (k_rolloutWs), 256 steps with autoresets: sampled oracle columns (reward codes, flags, final
   state, stats) and, for every env, the stats against the output traces.
+* c4 and c4c at the bench's exact launch shape, EVERY env against the C
+  oracle run in column shards on threads: c4 through the bench's own call
+  (sparc_rollout_obs_device -> k_rollout_obsw, 262,144 envs x 50 steps, max_steps 2,000, the
+  bench's action tiles), two back-to-back launches into the same [50][262,144][11][11] int32
+  traces (6.3 GB per plane, past 4 GiB: the size_t addressing of the writer waves), reward codes,
+  flags, stats, final state and every env's visited / agent_location planes at every step
+  (bit-packed losslessly on both sides after checking that every entry is 0 or 1); c4c through
+  sparc_rollout_device (k_rolloutWs, 262,144 envs x 2,000 steps, two launches).
 """
 import numpy as np
 import pytest
@@ -261,3 +269,112 @@ def test_c3_bench_kernel_exact_instantiation_full_size(on_gpu):
     f_all = f_np.reshape(-1, n)
     assert ((f_all & 1) != 0).sum() > 0 and ((f_all & 2) != 0).sum() > 0 and ((f_all & 64) != 0).sum() > 0
     assert int(ost[:, 2].sum()) > 0
+
+
+def _pack_planes_gpu(p):
+    """[T, N, X, Y] int32 planes on the GPU -> [T, N, ceil(X*Y/8)] uint8 on the host, bit c of a
+    row = entry c (np.packbits(..., bitorder='little') of the flattened plane); asserts that every
+    entry is 0 or 1, so the packing is lossless."""
+    T, N = p.shape[:2]
+    XY = p.shape[2] * p.shape[3]
+    nb = (XY + 7) // 8
+    w = (1 << torch.arange(8, device=p.device, dtype=torch.int32))
+    out = torch.empty((T, N, nb), dtype=torch.uint8, device=p.device)
+    for t in range(T):
+        f = p[t].reshape(N, XY)
+        assert bool(((f == 0) | (f == 1)).all())
+        f = torch.nn.functional.pad(f, (0, nb * 8 - XY)).view(N, nb, 8)
+        out[t] = (f * w).sum(-1).to(torch.uint8)
+    return out.cpu().numpy()
+
+
+def _pack_planes_np(v):
+    T, n = v.shape[:2]
+    return np.packbits(v.reshape(T, n, -1) != 0, axis=-1, bitorder="little")
+
+
+class _ShardedOracle:
+    """The C oracle over column shards of n envs in threads (ctypes and np.packbits release the
+    GIL), drawing the bench's counter-based actions (sparc_rand_action(seed, env, t)) itself."""
+
+    def __init__(self, proc, pids, tb, ms, shards=16):
+        from concurrent.futures import ThreadPoolExecutor
+        from oracle import OraclePool
+        self.n = len(pids)
+        self.bounds = np.linspace(0, self.n, shards + 1).astype(int)
+        opool = OraclePool(_oracle_pool(proc))
+        self.oracles = [COracle(opool, int(b - a), tb, ms, autoreset=1)
+                        for a, b in zip(self.bounds[:-1], self.bounds[1:])]
+        self.stats = [np.zeros((o.n, 4), np.int32) for o in self.oracles]
+        for o, a in zip(self.oracles, self.bounds[:-1]):
+            o.reset(pids[a:a + o.n])
+        self.ex = ThreadPoolExecutor(shards)
+
+    def launch(self, T, seed, t0, obs=None):
+        """One launch of T steps: (codes, flags) [T, n], and with obs = (X, Y) the packed planes."""
+        def one(k):
+            o, a, st = self.oracles[k], int(self.bounds[k]), self.stats[k]
+            if obs is None:
+                return o.rollout(T, None, seed, a, t0, st)
+            r, f, vo, ao = o.rollout_obs(T, obs[0], obs[1], None, seed, a, t0, st)
+            return r, f, _pack_planes_np(vo), _pack_planes_np(ao)
+        res = list(self.ex.map(one, range(len(self.oracles))))
+        return [np.concatenate([r[j] for r in res], 1) for j in range(len(res[0]))]
+
+    def final(self):
+        self.ex.shutdown()
+        states = [o.state() for o in self.oracles]
+        return np.concatenate(self.stats), {k: np.concatenate([s[k] for s in states]) for k in states[0]}
+
+
+@pytest.mark.parametrize("config", ["c4", "c4c"])
+def test_c4_bench_launch_shape_every_env(on_gpu, config):
+    """c4 / c4c exactly as bench.py runs them (262,144 envs of the mixed 5x5-11x11 pool, 1,024
+    puzzles, traceback, max_steps 2,000, next-step autoreset, the bench's action tiles
+    sparc_rand_action(ACTION_SEED, env, j * T + t) in HBM, T = 50 with planes / 2,000 without),
+    two back-to-back launches through the bench's C-ABI call with the state carried through HBM.
+    Every env's reward codes, flags, stats and final state, and with c4 every env's planes at
+    every step, equal the C oracle (SPaRC_Gym.py:956-979, 1111-1238)."""
+    import bench
+    from sparc_gym_amd import SPaRCVecEnv
+    sizes, full, tb, obs = bench.CONFIGS[config]
+    proc, table = _bench_pool(sizes, full)
+    n, L = 262144, 2
+    T = 50 if obs else 2000
+    pids = _bench_pids(n)
+    v = SPaRCVecEnv(n, processed=proc, table=table, traceback=tb, max_steps=2000, autoreset="next_step",
+                    observation="compact")
+    v.reset(options={"puzzle_index": pids})
+    X, Y = v.x_dim, v.y_dim
+    assert (X, Y) == (11, 11) and table.words == 2
+    dev = torch.device("cuda", 0)
+    acts = torch.empty((L, T, n), dtype=torch.uint8, device=dev)
+    for j in range(L):
+        v.random_actions(T, seed=bench.ACTION_SEED, t0=j * T, out=acts[j])
+    rew = torch.empty((L, T, n), dtype=torch.int8, device=dev)
+    flg = torch.empty((L, T, n), dtype=torch.uint8, device=dev)
+    stats = torch.zeros((n, 4), dtype=torch.int32, device=dev)
+    if obs:   # the bench's traces, reused by both launches: 6.3 GB per plane
+        ovis = torch.empty((T, n, X, Y), dtype=torch.int32, device=dev)
+        oag = torch.empty_like(ovis)
+        assert ovis.numel() * 4 > 4 * 2**30
+    ora = _ShardedOracle(proc, pids, tb, 2000)
+    v._stream()
+    for k in range(L):
+        if obs:
+            v.core.rollout_obs_device(T, acts[k].data_ptr(), rew[k].data_ptr(), flg[k].data_ptr(), stats.data_ptr(),
+                                      ovis.data_ptr(), oag.data_ptr(), X, Y)
+        else:
+            v.core.rollout_device(T, acts[k].data_ptr(), rew[k].data_ptr(), flg[k].data_ptr(), stats.data_ptr())
+        torch.cuda.synchronize()
+        out = ora.launch(T, bench.ACTION_SEED, k * T, (X, Y) if obs else None)
+        assert np.array_equal(rew[k].cpu().numpy(), out[0]), f"reward codes differ in launch {k}"
+        assert np.array_equal(flg[k].cpu().numpy(), out[1]), f"flags differ in launch {k}"
+        if obs:
+            assert np.array_equal(_pack_planes_gpu(ovis), out[2]), f"visited planes differ in launch {k}"
+            assert np.array_equal(_pack_planes_gpu(oag), out[3]), f"agent planes differ in launch {k}"
+    ost, so = ora.final()
+    assert np.array_equal(stats.cpu().numpy(), ost)
+    _state_equal(v.state(), so, table)
+    f_all = flg.cpu().numpy().reshape(-1, n)
+    assert ((f_all & 1) != 0).sum() > 0 and ((f_all & 2) != 0).sum() > 0 and ((f_all & 64) != 0).sum() > 0

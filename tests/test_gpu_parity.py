@@ -597,3 +597,36 @@ def test_rollout_obs_writer_waves_equal_inline(on_gpu, name, tb, n):
     assert np.array_equal(sa, sb)
     for k in ("x", "y", "step", "path_len", "puzzle", "outcome", "visited"):
         assert np.array_equal(np.asarray(xa[k]), np.asarray(xb[k])), k
+
+
+@pytest.mark.parametrize("pad", [0, 2])
+def test_rollout_obs_writer_waves_padded_x_dim(on_gpu, pad):
+    """the bit-stream staging holds 64 envs x 64 W bits, so a multi-word pool
+    whose planes are padded past its largest lattice (x_dim > x_max: 13 x 11 = 143 cells > 128
+    board bits at W = 2) must take the LUT staging.  The writer-wave planes equal the inline
+    kernel's and, inside the lattice, the unpadded planes; the padding rows are zero."""
+    from sparc_gym_amd import SPaRCVecEnv
+    proc, table = _make("mixed_5_11", seed=41)
+    assert table.words == 2
+    n, T = 1280, 40
+    rng = np.random.default_rng(7)
+    pids = rng.integers(len(proc), size=n)
+    acts = torch.from_numpy(rng.integers(0, 5, size=(T, n)).astype(np.uint8)).cuda()
+    runs = []
+    for x_pad, inline in ((0, False), (pad, False), (pad, True)):
+        v = SPaRCVecEnv(n, processed=proc, table=table, traceback=True, max_steps=30, observation="new")
+        v.x_dim = table.x_max + x_pad
+        if inline:
+            v.core.set_variant(v.core.VARIANT_OBS_INLINE, 1)
+        v.reset(options={"puzzle_index": pids})
+        r = v.rollout(T, acts, obs=True)
+        runs.append({k: r[k].cpu().numpy() for k in ("reward_code", "flags", "visited", "agent_location")})
+    base, stream, inl = runs
+    for k in base:
+        assert np.array_equal(stream[k], inl[k]), k
+    X = table.x_max
+    for k in ("visited", "agent_location"):
+        assert np.array_equal(stream[k][:, :, :X], base[k]), k
+        assert not stream[k][:, :, X:].any(), k
+    for k in ("reward_code", "flags"):
+        assert np.array_equal(stream[k], base[k]), k
