@@ -156,7 +156,16 @@ def state_bytes_per_env(words, traceback):
     return 8 * words + (16 * words if traceback else 0) + 16
 
 
-def cpu_baseline_rules(proc, tb, max_steps, seconds):
+def cpu_procs(world, usable=None):
+    """CPU-baseline processes for a job of `world` GPUs: the host cores available to the job, one
+    GPU's 16-core share per rank (the GPU box's process rules), at most the cores this process may
+    run on."""
+    if usable is None:
+        usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return max(1, min(16 * max(1, int(world)), int(usable)))
+
+
+def cpu_baseline_rules(proc, tb, max_steps, seconds, procs=0):
     """The reference-speed full step() including its rule audit: oracle/cpu_ref.py's step core +
     oracle/rules_ref.py's _validate_rules restatement TWICE per step, as the reference runs it
     (SPaRC_Gym.py:1227 with the step's flags, and 1011 in _get_info with both False), pure
@@ -201,7 +210,7 @@ def cpu_baseline_rules(proc, tb, max_steps, seconds):
            "value_1core": round(k / dt, 1),
            "value_1core_audit_once": round(k1 / dt1, 1)}
     # the same on one process per core of this GPU's share of the host (BASELINE.md's plan)
-    mp_ = _cpu_bench_multi("c3r", "py_rules", max_steps, seconds)
+    mp_ = _cpu_bench_multi("c3r", "py_rules", max_steps, seconds, procs)
     if mp_:
         out.update(value=mp_["value"], cores=mp_["procs"],
                    sample=out["sample"] + f"; value: {mp_['procs']} processes x 1 env, {mp_['seconds']:.0f} s "
@@ -209,7 +218,7 @@ def cpu_baseline_rules(proc, tb, max_steps, seconds):
     return out
 
 
-def cpu_baseline(proc, tb, max_steps, seconds, obs_dims=None, config="c3"):
+def cpu_baseline(proc, tb, max_steps, seconds, obs_dims=None, config="c3", procs=0):
     """C oracle (sparc_oracle.c, 1 thread) on a bounded sample of the same workload (with
     obs_dims = (x_dim, y_dim): also writing the 'new' observation planes of every step)."""
     from oracle import COracle
@@ -258,7 +267,8 @@ def cpu_baseline(proc, tb, max_steps, seconds, obs_dims=None, config="c3"):
     # the same oracle, one process per core (BASELINE.md CPU-baseline plan), in a child process
     # that never touches the GPU; up to 16 cores (one GPU's share of the box)
     cmd = [sys.executable, "-m", "oracle.cpu_bench", "--config", config, "--seconds", str(seconds),
-           "--max-steps", str(max_steps)] + (["--obs", str(obs_dims[0]), str(obs_dims[1])] if obs_dims else [])
+           "--max-steps", str(max_steps), "--procs", str(procs)] + \
+        (["--obs", str(obs_dims[0]), str(obs_dims[1])] if obs_dims else [])
     try:
         r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=seconds * 4 + 120)
         mc = json.loads(r.stdout.strip().splitlines()[-1])
@@ -266,11 +276,11 @@ def cpu_baseline(proc, tb, max_steps, seconds, obs_dims=None, config="c3"):
         out.update(value=mc["value"], cores=mc["procs"],
                    sample=out["sample"] +
                    f"; value: {mc['procs']} processes x {n} envs (oracle/cpu_bench.py), "
-                   f"{mc['seconds']:.0f} s, one per core of this GPU's share of the host",
+                   f"{mc['seconds']:.0f} s, one per core of the job's share of the host",
                    per_core=round(mc["value"] / mc["procs"], 1),
                    host={"physical_cores": phys, "logical_cpus": logical, "affinity_cpus": aff,
                          "cgroup_cpu_quota": quota,
-                         "note": "the GPU box gives one GPU's job a 16-core share (its process rules); "
+                         "note": "the GPU box gives a job a 16-core share per GPU (its process rules); "
                                  "whole_host_estimate = per_core x physical_cores is a linear estimate, "
                                  "not a measurement"})
         if phys:
@@ -278,7 +288,7 @@ def cpu_baseline(proc, tb, max_steps, seconds, obs_dims=None, config="c3"):
     except (subprocess.SubprocessError, ValueError, KeyError, IndexError) as exc:   # keep the 1-core number
         out["multi_core_error"] = repr(exc)[:200]
     if not obs_dims:   # the pure-Python port on the same cores (one process per core)
-        mp_ = _cpu_bench_multi(config, "py", max_steps, seconds)
+        mp_ = _cpu_bench_multi(config, "py", max_steps, seconds, procs)
         if mp_:
             out["python_port_multicore"] = {"value": mp_["value"], "procs": mp_["procs"],
                                             "sample": f"oracle/cpu_ref.py, {mp_['procs']} processes x 1 env, "
@@ -286,10 +296,10 @@ def cpu_baseline(proc, tb, max_steps, seconds, obs_dims=None, config="c3"):
     return out
 
 
-def _cpu_bench_multi(config, impl, max_steps, seconds):
+def _cpu_bench_multi(config, impl, max_steps, seconds, procs=0):
     """oracle/cpu_bench.py in a child process (never touches the GPU); its JSON or None."""
     cmd = [sys.executable, "-m", "oracle.cpu_bench", "--config", config, "--seconds", str(seconds),
-           "--max-steps", str(max_steps), "--impl", impl]
+           "--max-steps", str(max_steps), "--impl", impl, "--procs", str(procs)]
     try:
         r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=seconds * 4 + 120)
         return json.loads(r.stdout.strip().splitlines()[-1])
@@ -651,20 +661,24 @@ def main():
                                     f"{', exact-fit memo 48 B load+store' if memo_bytes else ''})"},
         "episodes": summary,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and rules:
-        cb = cpu_baseline_rules(proc, tb, args.max_steps, args.cpu_seconds)
-        out["cpu_baseline"] = cb
-        out["gpu_vs_cpu"] = round(value / cb["value"], 1)
-    elif rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb = cpu_baseline(proc, tb, args.max_steps, args.cpu_seconds, (X, Y) if obs else None, args.config)
+    if world > 1:
+        dist.destroy_process_group()
+    # the CPU step() beside the GPU number at EVERY world size (north_star: "next to the reference
+    # Python CPU step() timed on the host cores of the same box in the same run"): rank 0, after
+    # the timed region and the final barrier, on the host cores the job has (cpu_procs)
+    if rank == 0 and not args.no_cpu_baseline:
+        procs = cpu_procs(len(set(pci)))   # the GPUs the job drives (a rehearsal shares one)
+        if rules:
+            cb = cpu_baseline_rules(proc, tb, args.max_steps, args.cpu_seconds, procs)
+        else:
+            cb = cpu_baseline(proc, tb, args.max_steps, args.cpu_seconds, (X, Y) if obs else None, args.config,
+                              procs)
         out["cpu_baseline"] = cb
         out["gpu_vs_cpu"] = round(value / cb["value"], 1)
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -135,10 +135,12 @@ struct TrieLane {
     // (entry 4k + d = the record of node k's field-d node), the record the next step moves to IF
     // it moves along the trie: one unconditional 8-B gather per step whose data is used a whole
     // step later (the plain form's gather of the new node's own record is used half a step
-    // later).  It pays only while the L2 is lightly loaded (MI355X, 2,000-step launches: c2 at
-    // 4,096 envs 0.350 -> 0.337 ms; c3 at 65,536 envs 0.392 -> 0.410 ms, as 65,536 lanes then
-    // gather every step instead of on the rare node changes), so the host uses it for grids of
-    // at most 64 workgroups.
+    // later).  It pays only on small grids (MI355X, 2,000-step launches: c2 at 4,096 envs
+    // 0.350 -> 0.337 ms; c3 at 65,536 envs 0.392 -> 0.410 ms), so the host uses it for grids of at
+    // most 64 workgroups.  The c3 loss is not the L2 load of 65,536 lanes gathering every step: an
+    // exec-masked variant that gathers for on-trie lanes only costs the same 6-7 %
+    // (profiles/r05/ab_c3_la/); it is this form's per-step row read, selects and address on a
+    // SIMD the trie wave shares with the move wave, whose chain is the other half of the step.
     uint32_t nrx = ~0u, nry = ~0u;  // record of field[a] of the current node (a = this step's action)
 
     // the class byte of a step (CODES = false): min(S >> 15, 2) (0 on the trie, 1 on a solution,

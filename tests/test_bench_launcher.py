@@ -80,3 +80,24 @@ def test_rule_config_refuses_step_mode(monkeypatch, capsys):
         bench.parse()
     assert e.value.code == 2
     assert "c3r" in capsys.readouterr().err
+
+
+def test_cpu_baseline_cores_follow_the_job():
+    """rank 0 times the CPU step() after the timed region at every world size,
+    on the job's share of the host: 16 cores per GPU the job drives, at most the usable cores."""
+    assert bench.cpu_procs(1, usable=8) == 8
+    assert bench.cpu_procs(1, usable=256) == 16
+    assert bench.cpu_procs(2, usable=256) == 32
+    assert bench.cpu_procs(8, usable=256) == 128
+    assert bench.cpu_procs(8, usable=64) == 64
+
+
+def test_cpu_baseline_names_its_cores():
+    """The C-oracle baseline leg on a small sample with two processes: the record names the
+    processes it ran (cores) and the single-thread rate beside them."""
+    import os as _os
+    _os.environ["SPARC_POOL_WORKERS"] = "1"
+    proc = bench.make_pool(64, ((3, 3),), True)
+    cb = bench.cpu_baseline(proc, True, 2000, 0.5, None, "c3", procs=2)
+    assert cb["cores"] == 2 and cb["value"] > 0 and cb["value_1core"] > 0
+    assert "2 processes" in cb["sample"]

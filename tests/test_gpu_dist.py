@@ -49,8 +49,9 @@ def test_two_rank_hip_rollout_equals_single_process(on_gpu, tmp_path):
     assert got["stats"][:n, 1].sum() > 0 and got["stats"][n:, 1].sum() > 0
 
 
-def _bench_cmd(*extra):
-    return [sys.executable, os.path.join(os.path.dirname(HERE), "bench.py"), "--no-cpu-baseline",
+def _bench_cmd(*extra, cpu=False):
+    return [sys.executable, os.path.join(os.path.dirname(HERE), "bench.py"),
+            *(["--cpu-seconds", "1"] if cpu else ["--no-cpu-baseline"]),
             "--steps", "2", "--warmup", "1", "--env-steps", "64", "--envs", "4096"] + list(extra)
 
 
@@ -60,7 +61,7 @@ def test_bench_gpus2_launches_two_ranks_itself(on_gpu):
     world the ranks observed."""
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     env.pop("WORLD_SIZE", None)
-    r = subprocess.run(_bench_cmd("--gpus", "2", "--rehearsal", "--backend", "gloo"), env=env,
+    r = subprocess.run(_bench_cmd("--gpus", "2", "--rehearsal", "--backend", "gloo", cpu=True), env=env,
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     import json
@@ -73,6 +74,10 @@ def test_bench_gpus2_launches_two_ranks_itself(on_gpu):
     assert len(w["per_rank_kernel_ms"]) == 2 and all(t > 0 for t in w["per_rank_kernel_ms"])
     assert o["episodes"]["done"] > 0
     assert o["value"] > 0
+    # the CPU step() beside the GPU number at world 2 too (rank 0, after the timed region), on the
+    # job's share of the host: the one GPU both ranks drive -> at most 16 cores
+    cb = o["cpu_baseline"]
+    assert cb is not None and cb["value"] > 0 and 1 <= cb["cores"] <= 16, cb
 
 
 def test_bench_refuses_two_ranks_on_one_gpu(on_gpu):
