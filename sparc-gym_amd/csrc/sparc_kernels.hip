@@ -1094,7 +1094,9 @@ __device__ __forceinline__ void io_flush(IoCounters& ct, int32_t* cnt, uint32_t 
     ct = IoCounters{};
 }
 
-template <bool TB, bool RAND, bool LDS_TABLE, bool LA = false, bool IOR = false>
+// C: mixed trie tables, compact 4-B records for tries of at most 127 nodes (TrieLaneT<true>;
+// p.tab.trie8 / trow then point at trie4 / trow4)
+template <bool TB, bool RAND, bool LDS_TABLE, bool LA = false, bool IOR = false, bool C = false>
 __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, const uint8_t* __restrict__ act,
                                                         uint64_t seed, uint64_t t0, int8_t* __restrict__ rew,
                                                         uint8_t* __restrict__ flg, int4* __restrict__ stats) {
@@ -1283,8 +1285,12 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         // -> 0.266 ms per 1,000 steps with the earlier trie wave; with TrieLane, 2,000 steps:
         // 0.456 ms, 0.476 without priority, 0.477 with the move wave at 1 instead)
         __builtin_amdgcn_s_setprio(1);
-        TrieLane tl;
-        tl.load(p.st.pos[i], p.st.aux[i], p.st.pid[i], trow, p.tab.trie8, NP);
+        static_assert(!(C && LA), "compact records: the plain trie wave only");
+        using TL = TrieLaneT<C>;
+        using Rec = typename TL::Rec;
+        const Rec* trie = reinterpret_cast<const Rec*>(p.tab.trie8);
+        TL tl;
+        tl.load(p.st.pos[i], p.st.aux[i], p.st.pid[i], trow, trie, NP);
         const uint32_t* th = reinterpret_cast<const uint32_t*>(pb + kS_FH) + lane;
         uint8_t* tr = pb + kS_Rew + lane;
         static_assert(!(LA && RAND), "the look-ahead trie wave reads the next tile's actions from HBM tiles");
@@ -1318,9 +1324,9 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
 #pragma unroll
                 for (int j = 0; j < kGroup1s; ++j) {
                     int code;
-                    if constexpr (LA) code = tl.step1la<!IOR>(hb[j], av[j], av[j + 1], trow, p.tab.trieg, NP);
-                    else if constexpr (LDS_TABLE) code = tl.step1<!IOR>(hb[j], av[j], trow, p.tab.trie8, NP);
-                    else code = tl.step1s<!IOR, kRowSlots, kRowSlotStride>(hb[j], av[j], trow, p.tab.trie8, NP);
+                    if constexpr (LA) code = tl.template step1la<!IOR>(hb[j], av[j], av[j + 1], trow, p.tab.trieg, NP);
+                    else if constexpr (LDS_TABLE) code = tl.template step1<!IOR>(hb[j], av[j], trow, trie, NP);
+                    else code = tl.template step1s<!IOR, kRowSlots, kRowSlotStride>(hb[j], av[j], trow, trie, NP);
                     tr[(row0 + j) * 64] = (uint8_t)code;
                 }
             }
@@ -1330,9 +1336,9 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         if constexpr (IOR)   // the last step's hand-over word is still in the ring
             if (K > 0) tl.finish_oneg(th[((uint32_t)(K * kTile - 1) & (kRing - 1)) * 64u] & kHwDone);
         if constexpr (IOR) {
-            fin[0] = make_uint4(tl.S, (uint32_t)tl.Oneg, tl.pid, 0u);
+            fin[0] = make_uint4(tl.std_S(), (uint32_t)tl.Oneg, tl.pid, 0u);
         } else {
-            fin[0] = make_uint4(tl.S, (uint32_t)tl.Oneg, (uint32_t)tl.acc_x, tl.acc_z);
+            fin[0] = make_uint4(tl.std_S(), (uint32_t)tl.Oneg, (uint32_t)tl.acc_x, tl.acc_z);
             fin[1] = make_uint4(tl.acc_y, tl.pid, 0u, 0u);
         }
         __syncthreads();                                         // B_{K+2}
@@ -1888,6 +1894,11 @@ struct Ctx {
     uint4* t_row1 = nullptr;
     uint2* t_trie8 = nullptr;          // split-kernel tables (null: a puzzle's trie exceeds 15-bit nodes)
     uint2* t_trieg = nullptr;          // [nodes][4]: the record of each node's field-d node (k_rollout1s)
+    // mixed split tables (sparc_trie.hpp TrieLaneT<true>): 4-B records for tries of at most 127
+    // nodes, 8-B ones for the rest, byte-addressed, and their trie rows; taken by k_rollout1s on
+    // pools past the LDS row budget
+    uint8_t* t_trie4 = nullptr;
+    uint4* t_trow4 = nullptr;
     uint4 *t_trow = nullptr, *t_mrow = nullptr;
     // multi-word split kernel (k_rolloutWs): move rows and reset boards; split_w false when the
     // pool does not fit its layout (pitch > 15, LDS, or no trie8)
@@ -2185,7 +2196,7 @@ int sparc_destroy(void* ctx) {
     void* bufs[] = {c->vis, c->dirs, c->pos, c->aux, c->step, c->pid, c->t_open, c->t_info, c->t_root, c->t_trie, c->t_init, c->t_row1,
                     c->t_trie8, c->t_trow, c->t_mrow, c->t_mroww, c->t_boardw, c->err, c->s_act, c->s_flags, c->s_mask, c->s_rew, c->s_pidx, c->r_planes, c->r_inst_fc,
                     c->r_inst, c->r_shape_range, c->r_shape_area, c->r_shape_off, c->r_memo, c->s_bits, c->s_region, c->s_fit, c->r_reg_off, c->r_reg_tab, c->fq_count, c->fq_items, c->r_rows,
-                    c->t_trieg, c->d_hf};
+                    c->t_trieg, c->d_hf, c->t_trie4, c->t_trow4};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->snap) (void)hipFree(c->snap);
@@ -2282,6 +2293,10 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
     if (c->t_row1) HIPCHK(c, hipFree(c->t_row1));
     if (c->t_trie8) HIPCHK(c, hipFree(c->t_trie8));
     if (c->t_trieg) HIPCHK(c, hipFree(c->t_trieg));
+    if (c->t_trie4) HIPCHK(c, hipFree(c->t_trie4));
+    if (c->t_trow4) HIPCHK(c, hipFree(c->t_trow4));
+    c->t_trie4 = nullptr;
+    c->t_trow4 = nullptr;
     if (c->t_trow) HIPCHK(c, hipFree(c->t_trow));
     if (c->t_mrow) HIPCHK(c, hipFree(c->t_mrow));
     if (c->t_mroww) HIPCHK(c, hipFree(c->t_mroww));
@@ -2445,6 +2460,54 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
         HIPCHK(c, hipMemcpy(c->t_trieg, tg.data(), sizeof(uint2) * tg.size(), hipMemcpyHostToDevice));
         HIPCHK(c, hipMalloc(&c->t_trow, sizeof(uint4) * P));
         HIPCHK(c, hipMemcpy(c->t_trow, trow.data(), sizeof(uint4) * P, hipMemcpyHostToDevice));
+        // mixed tables (TrieLaneT<true>): a trie of at most 127 nodes as 4-B records (each 16-bit
+        // field of trie8 as an 8-bit one, index | terminal << 7, 0xFF none), a larger one as its
+        // 8-B records; each puzzle's records start on a 128-B line, the base is a byte offset, and
+        // bit 13 of the row's w marks a compact puzzle (root S then 0x80 / 0x100)
+        if (W == 1) {
+            std::vector<size_t> bo(P, 0);
+            size_t nb = 0;
+            auto tiny = [&](size_t q) { return (t->info[4 * q + 3] & 0xFFFFu) <= 127u; };
+            for (size_t q = 0; q < P; ++q) {
+                if (!((t->info[4 * q + 1] >> 16) & 2u)) continue;
+                nb = (nb + 127u) & ~(size_t)127u;
+                bo[q] = nb;
+                nb += (size_t)(t->info[4 * q + 3] & 0xFFFFu) * (tiny(q) ? 4u : 8u);
+            }
+            nb += 8;   // an 8-B gather of the last 4-B record stays in bounds
+            auto f8 = [](uint32_t f16) { return f16 == 0xFFFFu ? 0xFFu : (f16 & 0x7Fu) | ((f16 >> 15) << 7); };
+            auto rec4 = [&](uint2 r) {
+                return f8(r.x & 0xFFFFu) | (f8(r.x >> 16) << 8) | (f8(r.y & 0xFFFFu) << 16) | (f8(r.y >> 16) << 24);
+            };
+            std::vector<uint8_t> tb(nb, 0xFF);
+            std::vector<uint4> trow4(P);
+            for (size_t q = 0; q < P; ++q) {
+                const uint32_t cnt = t->info[4 * q + 3] & 0xFFFFu;
+                const bool rooted = (t->info[4 * q + 1] >> 16) & 2u, small4 = rooted && tiny(q);
+                const uint32_t w = trow[q].w;
+                uint2 root = make_uint2(trow[q].x, trow[q].y);
+                if (rooted) {
+                    for (uint32_t k = 0; k < cnt; ++k) {
+                        const uint2 r8 = t8[b8[q] + k];
+                        if (small4) {
+                            const uint32_t v = rec4(r8);
+                            memcpy(&tb[bo[q] + 4 * (size_t)k], &v, 4);
+                        } else {
+                            memcpy(&tb[bo[q] + 8 * (size_t)k], &r8, 8);
+                        }
+                    }
+                    if (small4) root = make_uint2(rec4(root), 0xFFFFFFFFu);
+                }
+                // root S 0x80 (terminal) / 0x100 (off the trie) in the compact layout
+                const uint32_t rs = small4 ? ((w & 0x10000u) ? 0x100u : ((w >> 15) & 1u) << 7) : (w & 0x18000u);
+                trow4[q] = make_uint4(root.x, root.y, (uint32_t)bo[q],
+                                      rs | (small4 ? 1u << 13 : 0u) | (w & 0x4000u) | (w & ~0x1FFFFu));
+            }
+            HIPCHK(c, hipMalloc(&c->t_trie4, nb));
+            HIPCHK(c, hipMemcpy(c->t_trie4, tb.data(), nb, hipMemcpyHostToDevice));
+            HIPCHK(c, hipMalloc(&c->t_trow4, sizeof(uint4) * P));
+            HIPCHK(c, hipMemcpy(c->t_trow4, trow4.data(), sizeof(uint4) * P, hipMemcpyHostToDevice));
+        }
         HIPCHK(c, hipMalloc(&c->t_mrow, sizeof(uint4) * P));
         HIPCHK(c, hipMemcpy(c->t_mrow, mrow.data(), sizeof(uint4) * P, hipMemcpyHostToDevice));
         // multi-word split geometry (sparc_movew.hpp): internal pitch + 1, the board plus a
@@ -2624,9 +2687,17 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
             const bool lds_s = kS_Base + sbytes <= budget;
             // past the row budget: rows from the L2, the trie rows handed over through slots
             const size_t shm_s = kS_Base + (lds_s ? sbytes : kS_SlotBytes);
+            // past the row budget the mixed tables (tries of at most 127 nodes in 4-B records:
+            // twice the nodes per L2 line; sparc_trie.hpp TrieLaneT<true>)
+            const bool compact = !lds_s && c->t_trie4;
+            Params ps = p;
+            if (compact) {
+                ps.tab.trie8 = reinterpret_cast<const uint2*>(c->t_trie4);
+                ps.tab.trow = c->t_trow4;
+            }
             auto launch_s = [&](auto kern, const uint8_t* a) {
                 if (shm_s > 64 * 1024 && (lds_rc = allow_big_lds(c, reinterpret_cast<const void*>(kern)))) return;
-                kern<<<dim3((unsigned)blocks), kBlock1s, shm_s, c->stream>>>(p, T16, a, seed, t0, d_rew, d_flags, st);
+                kern<<<dim3((unsigned)blocks), kBlock1s, shm_s, c->stream>>>(ps, T16, a, seed, t0, d_rew, d_flags, st);
             };
             // IOR (next-step autoreset): the I/O waves derive the reward codes and counters from
             // the trie wave's class bytes (io_codes4), which takes them off the trie wave's chain
@@ -2636,9 +2707,11 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
                     // look-ahead trie gathers on grids of at most 64 workgroups (sparc_trie.hpp)
                     if (lds_s && blocks <= 64) launch_s(k_rollout1s<TB, false, true, true, IOR>, d_act);
                     else if (lds_s) launch_s(k_rollout1s<TB, false, true, false, IOR>, d_act);
+                    else if (compact) launch_s(k_rollout1s<TB, false, false, false, IOR, true>, d_act);
                     else launch_s(k_rollout1s<TB, false, false, false, IOR>, d_act);
                 } else {
                     if (lds_s) launch_s(k_rollout1s<TB, true, true, false, IOR>, nullptr);
+                    else if (compact) launch_s(k_rollout1s<TB, true, false, false, IOR, true>, nullptr);
                     else launch_s(k_rollout1s<TB, true, false, false, IOR>, nullptr);
                 }
             };

@@ -20,6 +20,15 @@
 // node moves exactly in direction d_in ^ 2.  So forward move and pop are the same lookup,
 // field[action].
 //
+// Mixed tables (TrieLaneT<true>, k_rollout1s<…, C = true>: pools past the LDS row budget): a
+// puzzle whose trie has at most 127 nodes gets COMPACT records, 4 bytes per node, four 8-bit
+// fields (index | terminal << 7, 0xFF = none), and its lanes keep S = off << 8 | packed node; the
+// others keep the 8-B records.  The format is a per-lane register set at each reset (fm, from the
+// trie row), the transition the same with the field width, the perm selector, the key bound and
+// the depth / terminal shifts in registers, one shift more per step (the action's field offset).
+// Twice the nodes share an L2 line: the trie wave's record gathers are what misses the L2 on
+// pools whose records outgrow an XCD's 4 MB.
+//
 // Lane state: S = off << 16 | packed node (off = depth off the trie, 0 = on it), and Oneg =
 // the reward code a done step gets off a solution: -100, or 0 when the previous done step ended
 // with outcome_reward == 1 (1211: a post-done step then gets 0).  Everything is integer
@@ -37,8 +46,30 @@ namespace sparc {
 // per puzzle trie row: {root children right | up << 16, root children left | down << 16,
 // trie base, root S | has solutions << 14 | trie max << 17}; root S = 0 or 0x8000 ([start]
 // itself a solution) when some solution starts at start, else 0x10000 (off the trie from the
-// start).  Rootless: children 0xFFFF.
-struct TrieLane {
+// start).  Rootless: children 0xFFFF.  Mixed tables (C): the base is a BYTE offset, and a compact
+// puzzle's row holds {its root's 4-B record, ~0, base, root S (0, 0x80 or 0x100) | 1 << 13 | has
+// solutions << 14 | trie max << 17}.
+template <bool C = false>
+struct TrieLaneT {
+    typedef uint2 Rec;   // one 8-B load per gather (a compact record is its low half)
+    // S layout: node index below bit nb, terminal at bit nb, depth off the trie from bit os; wide
+    // records nb = 15, os = 16; compact (C, fm = 1) nb = 7, os = 8
+    uint32_t fm = 0, sh8 = 0;   // C: 1 compact / 0 wide, and fm << 3
+    // C: the record's bit offset in (ry:rx): a gather loads the 8-B aligned word holding the
+    // record, so an odd compact record sits in its high half (32); 0 otherwise
+    uint32_t hb = 0;
+    __device__ __forceinline__ uint32_t NB() const { return C ? 15u - sh8 : 15u; }
+    __device__ __forceinline__ uint32_t OS() const { return C ? 16u - sh8 : 16u; }
+    __device__ __forceinline__ uint32_t kNode() const { return C ? 0x7FFFu >> sh8 : 0x7FFFu; }
+    __device__ __forceinline__ uint32_t kKey() const { return C ? 0xFFFFu >> sh8 : 0xFFFFu; }
+    // the row's format (C): bit 13 of its w
+    __device__ __forceinline__ void set_format(uint32_t w) {
+        if constexpr (C) {
+            fm = __builtin_amdgcn_ubfe(w, 13u, 1u);
+            sh8 = fm << 3;
+        }
+    }
+    __device__ __forceinline__ uint32_t root_S(uint32_t w) const { return w & (0x18000u >> (C ? sh8 : 0u)); }
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
     typedef __attribute__((address_space(3))) v4u lds_v4;
     // row q of a row table (LDS or global) as one 4-vector, so that a read lands in one register tuple
@@ -48,7 +79,7 @@ struct TrieLane {
     }
     uint32_t S = 0;
     int32_t Oneg = -100;
-    uint32_t rx = ~0u, ry = ~0u;   // record of the current node (S & 0x7FFF)
+    uint32_t rx = ~0u, ry = ~0u;   // record of the current node (S & kNode(); compact: rx)
     uint32_t base = 0, tmax = 0;
     int32_t hs = 0, hsn = 0;        // the puzzle has solutions (the +-1 rewards apply, 1217); -hs
     uint32_t hsb = 0;               // hs << 2 (the class byte's bit 2, CODES = false)
@@ -60,12 +91,36 @@ struct TrieLane {
     __device__ __forceinline__ static uint32_t next_pid(uint32_t q, uint32_t num_puzzles) {
         return q + 1 == num_puzzles ? 0u : q + 1;   // reset() without options, SPaRC_Gym.py:1087
     }
+    __device__ __forceinline__ void set_rec(const uint2 r) {
+        rx = r.x;
+        ry = r.y;
+    }
+    // byte offset of node k's record (C: base is a byte offset, the record 4 or 8 B)
+    __device__ __forceinline__ uint32_t rec_off(uint32_t k) const {
+        if constexpr (C) return base + (k << (3u - fm));
+        return (base + k) << 3;
+    }
+    // the record of node k into (ry:rx) (C: the aligned 8-B word holding it, and hb)
+    __device__ __forceinline__ void fetch(const Rec* __restrict__ trie8, uint32_t k) {
+        const uint32_t o = rec_off(k);
+        if constexpr (C) {
+            set_rec(ld_off(trie8, o & ~7u));
+            hb = (o & 4u) << 3;
+        } else {
+            set_rec(ld_off(trie8, o));
+        }
+    }
+    // S in the SoA state's layout (off << 16 | terminal << 15 | node), for the launch-end hand-off
+    __device__ __forceinline__ uint32_t std_S() const {
+        if constexpr (!C) return S;
+        return ((S >> OS()) << 16) | (((S >> NB()) & 1u) << 15) | (S & kNode());
+    }
 
     // state at the start of a launch: the SoA record (pos: off in bits 24-31; aux: node,
     // outcome << 16 (1: +1), node_term << 19), the node's record and the next puzzle's row
     template <class Rows>
     __device__ __forceinline__ void load(const uint32_t ps, const uint32_t ax, const uint32_t q, const Rows& trow,
-                                         const uint2* __restrict__ trie8, uint32_t num_puzzles) {
+                                         const Rec* __restrict__ trie8, uint32_t num_puzzles) {
         pid = q;
         const uint4 r = trow[q];
         base = r.z;
@@ -73,13 +128,12 @@ struct TrieLane {
         hs = (int32_t)((r.w >> 14) & 1u);
         hsn = -hs;
         hsb = (uint32_t)hs << 2;
-        S = ((ps >> 24) << 16) | (ax & 0x7FFFu) | (((ax >> 19) & 1u) << 15);
+        set_format(r.w);
+        S = ((ps >> 24) << OS()) | (ax & 0x7FFFu) | (((ax >> 19) & 1u) << NB());
         Oneg = ((ax >> 16) & 3u) == 1u ? 0 : -100;
-        if ((r.w & 0x10000u) == 0u) {   // rootless puzzles keep off >= 1: the record is never read
+        if ((r.w & (1u << OS())) == 0u) {   // rootless puzzles keep off >= 1: the record is never read
             const uint32_t node = ax & 0x7FFFu;
-            const uint2 rec = trie8[base + (node < tmax ? node : tmax)];
-            rx = rec.x;
-            ry = rec.y;
+            fetch(trie8, node < tmax ? node : tmax);
         }
         npid = next_pid(q, num_puzzles);
         nx = row4(trow, npid);
@@ -102,7 +156,7 @@ struct TrieLane {
     }
     template <bool CODES, uint32_t SLOTS, uint32_t STRIDE, class Rows>
     __device__ __forceinline__ int step1s(const uint32_t hw, const uint32_t a16, const Rows& trow,
-                                          const uint2* __restrict__ trie8, uint32_t num_puzzles) {
+                                          const Rec* __restrict__ trie8, uint32_t num_puzzles) {
         const bool reset = hw_reset(hw);
         if (reset) {
             const bool fb = nres >= lim;
@@ -122,8 +176,10 @@ struct TrieLane {
     __device__ __forceinline__ void apply_row(const uint4 r) {
         rx = r.x;
         ry = r.y;
+        hb = 0;
         base = r.z;
-        S = r.w & 0x18000u;
+        set_format(r.w);
+        S = root_S(r.w);
         hs = (int32_t)((r.w >> 14) & 1u);
         hsn = -hs;
         hsb = (uint32_t)hs << 2;
@@ -150,7 +206,7 @@ struct TrieLane {
     __device__ __forceinline__ uint32_t class_byte(uint32_t x) const { return (x < 2u ? x : 2u) | hsb; }
     // Oneg after the launch's last step (CODES = false): 0 iff that step was done on a solution
     __device__ __forceinline__ void finish_oneg(uint32_t last_hw_done) {
-        Oneg = (last_hw_done != 0u && (S >> 15) == 1u) ? 0 : -100;
+        Oneg = (last_hw_done != 0u && (S >> NB()) == 1u) ? 0 : -100;
     }
 
     // after load(): the first step's look-ahead record (a016: its action << 4)
@@ -207,7 +263,7 @@ struct TrieLane {
     // stores the trie wave's actions that way, k_rollout1s)
     template <bool CODES = true, class Rows>
     __device__ __forceinline__ int step1(const uint32_t hw, const uint32_t a16, const Rows& trow,
-                                         const uint2* __restrict__ trie8, uint32_t num_puzzles) {
+                                         const Rec* __restrict__ trie8, uint32_t num_puzzles) {
         if (hw_reset(hw)) reset_from_nx<CODES>(trow, num_puzzles);
         if (walk1(hw, a16)) gather(trie8);
         return finish<CODES>(hw >= 0x40000000u, (hw & kHwDone) != 0u);
@@ -237,28 +293,28 @@ struct TrieLane {
     // the word clear (fwd - pop = 0), which keeps key above 0xFFFF as bit 16 does there, and the
     // depth step is (fwd - pop) << 16 from one arithmetic shift: field / key / depth in 8
     // instructions against 11 (the extraction of dd and of the not-moved bit)
+    //   C, compact lanes (fm = 1): the field is byte a16 / 16 of the 4-B record (the shift halved),
+    //   the perm selector takes one byte of it, the key bound is 0xFF and the depth sits at bit 8
     __device__ __forceinline__ bool walk1(const uint32_t hw, const uint32_t a16) {
         const uint64_t xy = ((uint64_t)ry << 32) | rx;
-        const uint32_t c = (uint32_t)(xy >> (a16 & 63u));           // a16 & 15 == 0: field a16 / 16
+        const uint32_t c = (uint32_t)(xy >> ((C ? (a16 >> fm) | hb : a16) & 63u));   // a16 & 15 == 0: field a16 / 16
         // field | S's depth half: one v_perm_b32 (the compiler's and / and / or3 took three)
-        const uint32_t key = __builtin_amdgcn_perm(S, c, 0x07060100u) | (~hw & 0x40000000u);
-        const bool take = key < 0xFFFFu;
+        const uint32_t key = __builtin_amdgcn_perm(S, c, C ? 0x07060100u + (fm << 10) : 0x07060100u) |
+                             (~hw & 0x40000000u);
+        const bool take = key < kKey();
         // fwd - pop by a signed field extract, shifted and added in one v_lshl_add_u32 (written
         // plainly, the compiler rewrote (hw >> 30) << 16 into a shift, a mask and an add)
         const int32_t dl = __builtin_amdgcn_sbfe((int32_t)hw, 30u, 2u);
         uint32_t Sm;
-        asm("v_lshl_add_u32 %0, %1, 16, %2" : "=v"(Sm) : "v"(dl), "v"(S));
+        if constexpr (C) asm("v_lshl_add_u32 %0, %1, %2, %3" : "=v"(Sm) : "v"(dl), "v"(OS()), "v"(S));
+        else asm("v_lshl_add_u32 %0, %1, 16, %2" : "=v"(Sm) : "v"(dl), "v"(S));
         S = take ? key : Sm;
         return take;
     }
     // the record changes only with the node (exec-masked gather; a random walk is off the trie on
     // most steps).  Every field of a record holds a node of the same puzzle (validated by
     // sparc_load_puzzles), so no clamp here; load() clamps the stored node.
-    __device__ __forceinline__ void gather(const uint2* __restrict__ trie8) {
-        const uint2 rec = ld_off(trie8, (base + (S & 0x7FFFu)) << 3);
-        rx = rec.x;
-        ry = rec.y;
-    }
+    __device__ __forceinline__ void gather(const Rec* __restrict__ trie8) { fetch(trie8, S & kNode()); }
     // autoreset step: the next puzzle's rows and its trie root
     template <bool CODES, class Rows>
     __device__ __forceinline__ void reset_from_nx(const Rows& trow, uint32_t num_puzzles) {
@@ -266,8 +322,10 @@ struct TrieLane {
         npid = next_pid(npid, num_puzzles);
         rx = nx.x;
         ry = nx.y;
+        hb = 0;
         base = nx.z;
-        S = nx.w & 0x18000u;
+        set_format(nx.w);
+        S = root_S(nx.w);
         hs = (int32_t)((nx.w >> 14) & 1u);
         hsn = -hs;
         hsb = (uint32_t)hs << 2;
@@ -287,7 +345,7 @@ struct TrieLane {
     // solutions (on / off the trie), else 0 (an autoreset step neither moves nor is done)
     template <bool CODES>
     __device__ __forceinline__ int finish(const bool moved, const bool done) {
-        const uint32_t x = S >> 15;                            // 0 on, 1 on a solution, >= 2 off
+        const uint32_t x = S >> NB();                          // 0 on, 1 on a solution, >= 2 off
         if constexpr (!CODES) return (int)class_byte(x);
         const int cd = x == 1u ? 100 : Oneg;
         const int cm = moved ? (x < 2u ? hs : hsn) : 0;
@@ -299,5 +357,6 @@ struct TrieLane {
         return code;
     }
 };
+using TrieLane = TrieLaneT<false>;
 
 }  // namespace sparc

@@ -85,8 +85,39 @@ def test_env_record_equals_separate_calls(on_gpu, name, tb, fit_cap):
         # the read entry point: no transition
         rec2 = a.env_read(audit=True)
         _check_record(rec2, table, b.read_state(), b.rules_host(region=True, fit=True))
-    if fit_cap == 1 and name != "7x7_full":   # (7 x 7 audits read the region-code table: no search)
-        assert host_fits > 0   # the host-finish path inside the call ran
+    # (whether the GPU's node cap queued searches depends on the episodes: the host-finish path
+    # inside the call is pinned by test_env_record_host_finish below)
+
+
+def test_env_record_host_finish(on_gpu):
+    """With the GPU's node cap at 1, the audit of a two-walled puzzle (test_gpu_rules_limits
+    _two_walls: two exact-fit searches per audit) queues both searches; sparc_env_reset /
+    sparc_env_step finish them on the host inside the call (host_fits = 2, no pending bit) and
+    the record equals the default cap's.  The host's answers are kept (HostFits): the next
+    audit of the same regions queues nothing."""
+    from test_gpu_rules_limits import _two_walls
+    recs = [r for r in map(_two_walls, synthetic.make_puzzles(40, seed=41, sizes=((7, 7),), full_properties=False,
+                                                               n_solutions=1)) if r is not None]
+    proc = process_puzzles(recs)
+    table, (a, _) = _cores(proc, True, 1)
+    _, (b, _) = _cores(proc, True, None)
+    ra = a.env_reset(0, audit=True)
+    rb = b.env_reset(0, audit=True)
+    assert ra.host_fits == 2 and rb.host_fits == 0
+    for r in (ra, rb):
+        assert r.audited == 1 and not r.rule_bits & (1 << 9)
+    assert (ra.rule_bits, ra.fit, bytes(ra.region)) == (rb.rule_bits, rb.fit, bytes(rb.region))
+    assert ra.fit & 1   # the left walled region (region 0) fits
+    again = a.env_reset(0, audit=True)
+    assert again.host_fits == 0 and (again.rule_bits, again.fit) == (ra.rule_bits, ra.fit)
+    rng = np.random.default_rng(2)
+    for _ in range(30):
+        act = int(rng.integers(4))
+        ra, rb = a.env_step(act, audit=True), b.env_step(act, audit=True)
+        assert (ra.rule_bits, ra.fit, bytes(ra.region), ra.flags) == (rb.rule_bits, rb.fit, bytes(rb.region), rb.flags)
+        assert not ra.rule_bits & (1 << 9)
+        if ra.flags & 3:
+            break
 
 
 def test_env_record_errors(on_gpu):

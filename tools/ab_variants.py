@@ -23,6 +23,20 @@ CSRC = os.path.join(REPO, "sparc-gym_amd", "csrc")
 VARIANTS = {
     # the in-tree sources, built the same way (the A/B baseline)
     "head": [],
+    # k_rollout1s: the I/O wave stores each lane's four target positions of a read
+    # group as one word ([group][lane][4 steps] bytes, 16 byte stores per tile), the move wave
+    # reads one ds_read_b32 per group and extracts byte j with v_bfe_u32, instead of four
+    # ds_read_u8 and their zero-extensions
+    "posword": [("sparc_kernels.hip", "                *reinterpret_cast<u32x4*>(smem + kS_Pos + o) = q;",
+                 """                {
+                    uint8_t* pq = smem + kS_Pos + io * kS_Pair + (k % 3) * (kTile * 64) + (r >> 2) * 256u + (r & 3u) + c * 4u;
+#pragma unroll
+                    for (int kk = 0; kk < 16; ++kk) pq[kk * 4] = (uint8_t)(q[kk >> 2] >> (8 * (kk & 3)));
+                }"""),
+                ("sparc_kernels.hip", "            const uint8_t* tp = pb + kS_Pos + (k % 3) * (kTile * 64) + lane;",
+                 "            const uint8_t* tp = pb + kS_Pos + (k % 3) * (kTile * 64) + lane * 4u;"),
+                ("sparc_kernels.hip", "                        pv[j] = tp[(g + j) * 64];",
+                 "                        pv[j] = __builtin_amdgcn_ubfe(*reinterpret_cast<const uint32_t*>(tp + g * 64), 8u * j, 8u);")],
     # k_rollout1r audit waves: region codes not looked up (a constant code instead of reg_tab)
     "notab": [("sparc_rules.hpp", "            tw = rt.reg_tab[(fo + m) >> 3];", "            tw = 0x55555555u;")],
     # k_rollout1r audit waves: the puzzle's rule data loaded once, not on every puzzle change
@@ -82,8 +96,8 @@ VARIANTS = {
                "__launch_bounds__(kBlockOw) __attribute__((amdgpu_waves_per_eu(8)))")],
     # k_rollout1s: trie wave at priority 2, move wave at 1, I/O waves at 0 (the I/O waves yield)
     "prio21": [("sparc_kernels.hip", """        __builtin_amdgcn_s_setprio(1);
-        TrieLane tl;""", """        __builtin_amdgcn_s_setprio(2);
-        TrieLane tl;"""),
+        static_assert(!(C && LA),""", """        __builtin_amdgcn_s_setprio(2);
+        static_assert(!(C && LA),"""),
                ("sparc_kernels.hip", """    if (wv < 4) {                                                // ---- move waves
         MoveLane1<TB> m;""", """    if (wv < 4) {                                                // ---- move waves
         __builtin_amdgcn_s_setprio(1);
@@ -102,7 +116,12 @@ VARIANTS = {
     "nola": [("sparc_kernels.hip", "if (lds_s && blocks <= 64) launch_s(k_rollout1s<TB, false, true, true, IOR>, d_act);",
               "if (lds_s && blocks <= 0) launch_s(k_rollout1s<TB, false, true, true, IOR>, d_act);")],
     "noprio": [("sparc_kernels.hip", """        __builtin_amdgcn_s_setprio(1);
-        TrieLane tl;""", """        TrieLane tl;""")],
+        static_assert(!(C && LA),""", """        static_assert(!(C && LA),""")],
+    # k_rollout1s on the mixed trie tables (compact 4-B records) although the rows fit LDS
+    "mixed": [("sparc_kernels.hip", """                    else if (lds_s) launch_s(k_rollout1s<TB, false, true, false, IOR>, d_act);""",
+               """                    else if (lds_s) launch_s(k_rollout1s<TB, false, true, false, IOR, true>, d_act);"""),
+              ("sparc_kernels.hip", """            const bool compact = !lds_s && c->t_trie4;""",
+               """            const bool compact = c->t_trie4 && !(lds_s && blocks <= 64);""")],
     # k_rollout1r with s_memtime stamps (timing only: the stats buffer receives, per wave, role |
     # total | barrier-wait | audit cycles at index N/2 + block * 16 + wave; tools/diag_r1r.py)
     "stamps": [

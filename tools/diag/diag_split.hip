@@ -10,7 +10,8 @@ __device__ __forceinline__ uint64_t stamp() { return __builtin_amdgcn_s_memtime(
 
 // TrieLane with the record gather replaced (G = 1: from an LDS table, valid memory but fake
 // records; G = 2: no gather, the record stays: timing only, the outputs are wrong; G = 3: the
-// current node's record reloaded every step, no exec-masked branch: correct)
+// current node's record reloaded every step, no exec-masked branch: correct; G = 4: the
+// product's step1 (walk1) with the gather left out: timing only)
 template <int G>
 struct DiagTrieLane : TrieLane {
     const uint4* lds_rows = nullptr;
@@ -20,6 +21,11 @@ struct DiagTrieLane : TrieLane {
     __device__ __forceinline__ int step1d(const uint32_t hw, const uint32_t a, const Rows& trow,
                                           const uint2* __restrict__ trie8, uint32_t num_puzzles) {
         if constexpr (G == 0) return step1<CODES>(hw, a, trow, trie8, num_puzzles);
+        if constexpr (G == 4) {   // the product's step1 without the record gather (timing only)
+            if (hw_reset(hw)) reset_from_nx<CODES>(trow, num_puzzles);
+            walk1(hw, a);
+            return finish<CODES>(hw >= 0x40000000u, (hw & kHwDone) != 0u);
+        }
         const bool reset = hw_reset(hw);
         const uint32_t dd = (uint32_t)((int32_t)hw >> 14) & 0xFFFF0000u;
         const bool moved = hw >= 0x40000000u, done = (hw & kHwDone) != 0u;
@@ -66,10 +72,55 @@ struct DiagTrieLane : TrieLane {
 
 // MoveLane1 with the autoreset variants: MV 0 the product's (divergent branch), 1 none (timing
 // only), 2 a wave-uniform branch around it (no exec save / restore when no lane resets), 4 the
-// branch without the next-row prefetch (timing only)
+// branch without the next-row prefetch (timing only); and the LDS-wait variants (timing only,
+// wrong outputs): 5 the target positions from registers instead of the I/O wave's LDS tile
+// (pos_v), 6 the stack byte of the next pop (pnr) from a register instead of an LDS read
 template <bool TB, int MV>
 struct DiagMoveLane1 : MoveLane1<TB> {
     using B = MoveLane1<TB>;
+    // the group's target position j (MV 5: a register pattern over the four window positions)
+    __device__ __forceinline__ uint32_t pos_v(const uint8_t* tp, uint32_t sj, uint32_t P) const {
+        if constexpr (MV == 5) {
+            const uint32_t a = (sj * 0x9E3779B1u + B::e * 7u) >> 30;
+            return a == 0 ? 2u * P : a == 1 ? P - 1u : a == 2 ? 0u : P + 1u;
+        }
+        return tp[sj * 64];
+    }
+    __device__ __forceinline__ uint32_t step_pos(const Params& p, uint32_t pos, bool rs) {
+        if constexpr (MV != 6) return B::step_pos(p, pos, rs);
+        // the product's step_pos with pnr kept in a register (no LDS read of slot len-3)
+        const uint32_t P = p.pitch;
+        B::step = __builtin_elementwise_add_sat(B::step, 1);
+        const bool trunc0 = B::step >= p.max_steps;
+        const uint32_t fwd = __builtin_amdgcn_ubfe(B::w, pos, 1u);
+        uint32_t pop = 0;
+        if constexpr (TB) pop = pos == B::rp ? B::bias : 0u;
+        const uint32_t moved = fwd | pop;
+        const int32_t d = (int32_t)pos - (int32_t)P;
+        uint32_t tog;
+        asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(tog) : "v"(fwd), "v"(d), "v"(B::e + P));
+        B::fr ^= (uint64_t)moved << (tog & 63u);
+        const int32_t dl = (int32_t)fwd - (int32_t)pop;
+        if constexpr (TB) {
+            const uint32_t arp = 2u * P - pos;
+            *B::lds_byte(B::sq + 128u) = (uint8_t)arp;
+            const uint32_t orp = B::rp;
+            B::rp = fwd ? arp : (pop ? B::pnr : B::rp);
+            B::sq += (uint32_t)dl << 6;
+            B::bias = (B::sq + B::bks) >> 31;
+            B::pnr = fwd ? orp : B::pnr;   // a register stand-in for slot len-3
+        } else {
+            B::len += fwd;
+        }
+        B::e = (uint32_t)((int32_t)B::e + __mul24((int32_t)moved, d));
+        B::w = (uint32_t)(B::fr >> (B::e & 63u));
+        uint32_t lw = B::w & p.nbm;
+        if constexpr (TB) lw |= B::bias << B::rp;
+        const bool at_tgt = B::e == B::tgt;
+        const bool done = trunc0 | (lw == 0u) | at_tgt;
+        B::pending = done & !rs;
+        return ((uint32_t)dl << 30) | ((at_tgt | rs) ? kHwTgt : 0u) | (B::pending ? kHwDone : 0u) | lw;
+    }
     __device__ __forceinline__ bool reset_v(const bool ar, const uint4* mrow, uint32_t col_addr) {
         if constexpr (MV == 0) {
             return B::reset_next(ar, mrow, col_addr);
@@ -141,11 +192,14 @@ extern "C" int sparc_diag_rollout1s(void* ctx, int32_t T, const uint8_t* d_act, 
             if (g == 1) go(k_rollout1s_diag<TB, false, true, 1, MV, false, true>);
             else if (g == 2) go(k_rollout1s_diag<TB, false, true, 2, MV, false, true>);
             else if (g == 3) go(k_rollout1s_diag<TB, false, true, 3, MV, false, true>);
+            else if (g == 4) go(k_rollout1s_diag<TB, false, true, 4, MV, false, true>);
             else go(k_rollout1s_diag<TB, false, true, 0, MV, false, true>);
         };
         if (mv == 1) pg(std::integral_constant<int, 1>{});
         else if (mv == 2) pg(std::integral_constant<int, 2>{});
         else if (mv == 4) pg(std::integral_constant<int, 4>{});
+        else if (mv == 5) pg(std::integral_constant<int, 5>{});
+        else if (mv == 6) pg(std::integral_constant<int, 6>{});
         else pg(std::integral_constant<int, 0>{});
     };
     if (c->cfg.traceback) pick(std::true_type{});
