@@ -117,6 +117,33 @@ VARIANTS = {
               "if (lds_s && blocks <= 0) launch_s(k_rollout1s<TB, false, true, true, IOR>, d_act);")],
     "noprio": [("sparc_kernels.hip", """        __builtin_amdgcn_s_setprio(1);
         static_assert(!(C && LA),""", """        static_assert(!(C && LA),""")],
+    # MoveLane1 (k_rollout1s move wave): the stack byte a pop needs (slot len-4) read one step
+    # ahead, off the chain; pnr (slot len-3) then follows by selects: a forward move makes it the
+    # old rp, a pop the prefetched byte, no move keeps it (the LDS read latency leaves the chain)
+    "pnrahead": [("sparc_move1.hpp", "    uint32_t rp = 0, pnr = 0;             // traceback: back position of the last move / the one before",
+                  "    uint32_t rp = 0, pnr = 0, pp = 0;     // traceback: back position of the last move / the one before"),
+                 ("sparc_move1.hpp", "            rp = fwd ? arp : (pop ? pnr : rp);",
+                  "            const uint32_t orp = rp;\n            rp = fwd ? arp : (pop ? pnr : rp);\n            pnr = fwd ? orp : (pop ? pp : pnr);"),
+                 ("sparc_move1.hpp", "        if constexpr (TB) pnr = *lds_byte(sq);",
+                  "        if constexpr (TB) pp = *lds_byte(sq - 64u);"),
+                 ("sparc_move1.hpp", "            pnr = *lds_byte(sq);\n",
+                  "            pnr = *lds_byte(sq);\n            pp = *lds_byte(sq - 64u);\n")],
+    # MoveLane1: at-target / no-legal-move / done / pending and the hand-over word's bits by VALU
+    # integer ops (x == 0 as (x - 1) >> 31) instead of v_cmp -> s_or / s_and -> v_cndmask chains
+    "valudone": [("sparc_move1.hpp", """        const bool at_tgt = e == tgt;                                                // 1192
+        const bool done = trunc0 | (lw == 0u) | at_tgt;                             // 1195-1199
+        // an autoreset step is never done (w = 0 before it: lw was 0) and reports at-target
+        pending = done & !rs;""", """        auto eq0 = [](uint32_t x) {   // 1 iff x == 0 (x < 2^31), VALU only
+            uint32_t r;
+            asm("v_add_u32 %0, -1, %1\\n\\tv_lshrrev_b32 %0, 31, %0" : "=&v"(r) : "v"(x));
+            return r;
+        };
+        const uint32_t at = eq0(e ^ tgt);
+        const uint32_t rsu = rs ? 1u : 0u;
+        const uint32_t pu = (at | eq0(lw) | (trunc0 ? 1u : 0u)) & (rsu ^ 1u);
+        pending = pu != 0u;"""),
+                 ("sparc_move1.hpp", "        return ((uint32_t)dl << 30) | ((at_tgt | rs) ? kHwTgt : 0u) | (pending ? kHwDone : 0u) | lw;",
+                  "        return ((uint32_t)dl << 30) | ((at | rsu) << 24) | (pu << 25) | lw;")],
     # k_rollout1s on the mixed trie tables (compact 4-B records) although the rows fit LDS
     "mixed": [("sparc_kernels.hip", """                    else if (lds_s) launch_s(k_rollout1s<TB, false, true, false, IOR>, d_act);""",
                """                    else if (lds_s) launch_s(k_rollout1s<TB, false, true, false, IOR, true>, d_act);"""),
