@@ -34,7 +34,7 @@ import numpy as np
 
 from .core import SparcCore
 from .puzzles import pack_rules, pack_table, process_puzzles
-from .rules import region_map_of, rule_status as _rule_status
+from .rules import RuleStatic, region_map_of, rule_status as _rule_status
 from .spaces import Box, Dict, Discrete, Env, Text
 
 _REWARD = {0: 0, 1: 0.01, -1: -0.01, 100: 1, -100: -1}   # code -> the reference's Python value
@@ -139,6 +139,7 @@ class SPaRC_Gym(Env):
         self._legal = 0
         self._rec = None          # the last one-env record (sparc_env_*), its audit for _validate_rules
         self._bit_index = {}      # (x_size, y_size) -> visited-board word / bit of every plane cell
+        self._rstatic = {}        # puzzle index -> rules.RuleStatic (what rule_status reads of the puzzle)
         self._load_puzzle(self.current_puzzle_index)
         self._validate_rules()                                                       # 182
 
@@ -359,9 +360,13 @@ class SPaRC_Gym(Env):
                 rp["bits"][0] = bits
                 r = rp
         rmap = region_map_of(r["region"][0], self.x_size, self.y_size, self._core.table.pitch)
-        self.rule_status = _rule_status(self.puzzles[self.current_puzzle_index], self.obs_array, self.path,
-                                        self._agent_location, self._target_location, r["bits"][0], rmap,
-                                        r["fit"][0], terminated, truncated)
+        q = self.current_puzzle_index
+        st = self._rstatic.get(q)
+        if st is None:
+            st = self._rstatic[q] = RuleStatic(self.puzzles[q], self.obs_array)
+        self.rule_status = _rule_status(self.puzzles[q], self.obs_array, self.path, self._agent_location,
+                                        self._target_location, r["bits"][0], rmap, r["fit"][0], terminated,
+                                        truncated, static=st)
         return self.rule_status
 
     def _get_legal_actions(self):

@@ -27,35 +27,66 @@ def region_map_of(region_bits, x_size, y_size, pitch):
     return np.where(r == 255, -1, r)
 
 
+class RuleStatic:
+    """What rule_status reads of a puzzle that no step changes, as plain Python lists (numpy
+    scalar indexing per cell cost most of a call): the symbol cells of each layer in the
+    reference's iteration order (obs_array layer order, x-major), the colour grid, the
+    triangle cells with their required counts, the dot cells, the gap grid and the poly / ylop
+    instances (_extract_poly_instances, SPaRC_Gym.py:714-734)."""
+
+    def __init__(self, puzzle, obs_array):
+        self.color = np.asarray(puzzle["color_array"]).tolist()
+        add = np.asarray(puzzle["additional_info"])
+        self.layers = []
+        for layer, arr in obs_array.items():
+            if layer in SKIP_LAYERS:
+                continue
+            xs, ys = np.where(np.asarray(arr) == 1)
+            self.layers.append((layer, list(zip(xs.tolist(), ys.tolist()))))
+        self.keys = set(obs_array.keys())
+        self.gaps = np.asarray(obs_array["gaps"]).tolist()
+        self.dots = None
+        if "dot" in obs_array:
+            xs, ys = np.where(np.asarray(obs_array["dot"]) == 1)
+            self.dots = list(zip(xs.tolist(), ys.tolist()))
+        self.tri = None
+        if "triangle" in obs_array:
+            tri = np.asarray(obs_array["triangle"])
+            h, w = tri.shape
+            self.tri = [(x, y, int(add[x, y])) for x in range(1, h - 1) for y in range(1, w - 1)
+                        if tri[x, y] == 1 and int(add[x, y]) > 0]
+        self.inst = _poly_instances(puzzle, obs_array, add)
+
+
 def rule_status(puzzle, obs_array, path, agent, target, bits, region_map, fit, terminated=False,
-                truncated=False):
+                truncated=False, static=None):
     """The reference's rule_status dict (structure of SPaRC_Gym.py:896-950).
 
     The GPU caps each exact-fit search; the C ABI finishes any search past the cap on the host
     without a cap (sparc_rules_finish, run by sparc_rules_host), so `bits` always carry the
-    reference's answer.  Bits that still mark a pending search are a caller error."""
+    reference's answer.  Bits that still mark a pending search are a caller error.  static: the
+    puzzle's RuleStatic (built here when not given; SPaRC_Gym keeps one per puzzle)."""
     if int(bits) & RULE_SEARCH_EXHAUSTED:
         raise RuntimeError("rule bits with a pending exact-fit search: call sparc_rules_finish first")
-    color = np.asarray(puzzle["color_array"])
-    add = np.asarray(puzzle["additional_info"])
+    st = static if static is not None else RuleStatic(puzzle, obs_array)
+    color = st.color
     passed = {n: bool((int(bits) >> k) & 1) for k, n in enumerate(RULE_NAMES)}
-    nreg = int(region_map.max()) + 1 if region_map.size and region_map.max() >= 0 else 0
+    rm = np.asarray(region_map)
+    rml = rm.tolist()
+    nreg = int(rm.max()) + 1 if rm.size and rm.max() >= 0 else 0
     # _collect_region_symbols (456-481): per region, layer -> coords and colour -> count
     symbols = [dict() for _ in range(nreg)]
     colors = [dict() for _ in range(nreg)]
-    for layer, arr in obs_array.items():
-        if layer in SKIP_LAYERS:
-            continue
-        xs, ys = np.where(np.asarray(arr) == 1)
-        for x, y in zip(xs, ys):
-            rid = region_map[x, y]
+    for layer, cells in st.layers:
+        for x, y in cells:
+            rid = rml[x][y]
             if rid == -1:
                 continue
             symbols[rid].setdefault(layer, []).append((x, y))
-            c = color[x, y]
+            c = color[x][y]
             if c:
                 colors[rid][c] = colors[rid].get(c, 0) + 1
-    area = [int((region_map == r).sum()) for r in range(nreg)]
+    area = np.bincount(rm[rm >= 0], minlength=nreg).tolist() if nreg else []
     res = {}
 
     def add_rule(name, detail):
@@ -64,15 +95,15 @@ def rule_status(puzzle, obs_array, path, agent, target, bits, region_map, fit, t
     add_rule("reached_target", {"agent_loc": np.asarray(agent).tolist(), "target_loc": np.asarray(target).tolist()})
     counts = Counter(tuple(p) for p in path)
     add_rule("path_not_crossing", {"duplicates": {k: v for k, v in counts.items() if v > 1}})
-    gaps = obs_array["gaps"]
-    add_rule("no_gap_violations", {"violations": [(x, y) for x, y in path if gaps[x, y] == 1]})
-    if "dot" not in obs_array:
+    gaps = st.gaps
+    add_rule("no_gap_violations", {"violations": [(x, y) for x, y in path if gaps[x][y] == 1]})
+    if st.dots is None:
         add_rule("all_dots_collected", {"total": 0, "collected": 0})
     else:
-        dot = np.asarray(obs_array["dot"]) == 1
-        add_rule("all_dots_collected", {"total": int(dot.sum()),
-                                        "collected": int((dot & (np.asarray(obs_array["visited"]) == 1)).sum())})
-    if "square" not in obs_array:
+        vis = obs_array["visited"]
+        add_rule("all_dots_collected", {"total": len(st.dots),
+                                        "collected": sum(1 for x, y in st.dots if vis[x, y] == 1)})
+    if "square" not in st.keys:
         add_rule("square_color_separation", {"regions": []})
     else:
         bad, det = [], []
@@ -80,12 +111,12 @@ def rule_status(puzzle, obs_array, path, agent, target, bits, region_map, fit, t
             sq = symbols[r].get("square", [])
             if not sq:
                 continue
-            cs = set(color[x, y] for x, y in sq if color[x, y] != 0)
+            cs = set(color[x][y] for x, y in sq if color[x][y] != 0)
             if len(cs) > 1:
                 bad.append(r)
             det.append({"region": r, "square_count": len(sq), "colors": list(cs)})
         add_rule("square_color_separation", {"violating_regions": bad, "region_square_details": det})
-    if "star" not in obs_array:
+    if "star" not in st.keys:
         add_rule("star_pairing_exact", {"regions": []})
     else:
         viol, per = [], []
@@ -96,12 +127,12 @@ def rule_status(puzzle, obs_array, path, agent, target, bits, region_map, fit, t
             allc = {}
             for coords in symbols[r].values():
                 for x, y in coords:
-                    c = color[x, y]
+                    c = color[x][y]
                     if c != 0:
                         allc[c] = allc.get(c, 0) + 1
             sc = {}
             for x, y in stars:
-                c = color[x, y]
+                c = color[x][y]
                 if c == 0:
                     viol.append({"region": r, "color": 0, "found_total": 1})
                     continue
@@ -116,24 +147,17 @@ def rule_status(puzzle, obs_array, path, agent, target, bits, region_map, fit, t
                 det.append({"color": c, "total_symbols_of_color": tot, "star_cells": n, "ok": ok})
             per.append({"region": r, "details": det, "all_ok": ok_all})
         add_rule("star_pairing_exact", {"violations": viol, "per_region": per})
-    if "triangle" not in obs_array:
+    if st.tri is None:
         add_rule("triangles_edge_count", {"mismatches": []})
     else:
-        tri = np.asarray(obs_array["triangle"])
-        h, w = tri.shape
         nodes = {(p[0], p[1]) for p in path}
         mism = []
-        for x in range(1, h - 1):
-            for y in range(1, w - 1):
-                if tri[x, y] == 1:
-                    req = int(add[x, y])
-                    if req <= 0:
-                        continue
-                    t = sum(1 for q in ((x + 1, y), (x - 1, y), (x, y - 1), (x, y + 1)) if q in nodes)
-                    if t != req:
-                        mism.append({"x": x, "y": y, "required": req, "touches": t})
+        for x, y, req in st.tri:
+            t = ((x + 1, y) in nodes) + ((x - 1, y) in nodes) + ((x, y - 1) in nodes) + ((x, y + 1) in nodes)
+            if t != req:
+                mism.append({"x": x, "y": y, "required": req, "touches": t})
         add_rule("triangles_edge_count", {"mismatches": mism})
-    add_rule("poly_ylop_area", _poly_detail(puzzle, obs_array, add, region_map, area, fit))
+    add_rule("poly_ylop_area", _poly_detail(st.inst, rml, area, fit))
     core = [k for k in res]
     add_rule("all_rules_satisfied", {"rules_checked": core})
     res["_terminated"] = {"passed": True, "detail": terminated}
@@ -143,8 +167,8 @@ def rule_status(puzzle, obs_array, path, agent, target, bits, region_map, fit, t
     return res
 
 
-def _poly_detail(puzzle, obs_array, add, region_map, area, fit):
-    """_rule_poly_ylop_balance (648-709) detail; the area check and exact fit come from the GPU."""
+def _poly_instances(puzzle, obs_array, add):
+    """The poly / ylop instances of _rule_poly_ylop_balance (714-734): name, cell, area, kind."""
     shapes = puzzle["polyshapes"]
     inst = []
     if isinstance(shapes, dict):
@@ -157,11 +181,16 @@ def _poly_detail(puzzle, obs_array, add, region_map, area, fit):
                     a = int(np.array(shapes[name]).sum())
                     kind = "poly" if obs_array["poly"][x, y] == 1 else "ylop"
                     inst.append({"name": name, "x": x, "y": y, "area": a, "kind": kind})
+    return inst
+
+
+def _poly_detail(inst, rml, area, fit):
+    """_rule_poly_ylop_balance (648-709) detail; the area check and exact fit come from the GPU."""
     if not inst:
         return {"regions": []}
     by_region = {}
     for it in inst:
-        rid = region_map[it["x"], it["y"]]
+        rid = rml[it["x"]][it["y"]]
         if rid != -1:
             by_region.setdefault(int(rid), []).append(it)
     details = []
