@@ -348,9 +348,13 @@ int sparc_set_rule_limits(void *ctx, uint32_t fit_cap_nodes, uint64_t table_entr
  *                                      1 <4, 3, 12>, 2 <2, 4, 12>
  *  SPARC_VARIANT_OBS_INLINE            1: sparc_rollout_obs_device on the per-wave kernel that
  *                                      writes its own planes; 0: default (writer waves)
+ *  SPARC_VARIANT_MIXED_TRIE            W = 1 pools past the LDS row budget: the split kernel on
+ *                                      the mixed trie tables (4-B records for tries of <= 127
+ *                                      nodes) 0: when the 8-B records outgrow 4 MB (default),
+ *                                      1: always, 2: never
  * SPARC_E_INVALID for another `which` or value. */
 enum { SPARC_VARIANT_IO_CODES_OFF = 1, SPARC_VARIANT_RULE_ROLLOUT_GENERIC = 2, SPARC_VARIANT_R1R_SHAPE = 3,
-       SPARC_VARIANT_OBS_INLINE = 4 };
+       SPARC_VARIANT_OBS_INLINE = 4, SPARC_VARIANT_MIXED_TRIE = 5 };
 int sparc_set_variant(void *ctx, int32_t which, int32_t value);
 
 /* ---- multi-GPU: the end-of-batch gather over RCCL (xGMI) -------------------------------------

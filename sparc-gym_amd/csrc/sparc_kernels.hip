@@ -1096,8 +1096,11 @@ __device__ __forceinline__ void io_flush(IoCounters& ct, int32_t* cnt, uint32_t 
 
 // C: mixed trie tables, compact 4-B records for tries of at most 127 nodes (TrieLaneT<true>;
 // p.tab.trie8 / trow then point at trie4 / trow4)
-template <bool TB, bool RAND, bool LDS_TABLE, bool LA = false, bool IOR = false, bool C = false>
-__global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, const uint8_t* __restrict__ act,
+// PR: move / trie wave pairs per workgroup (64 envs each), with PR I/O waves: 4 (256 envs, 12 waves:
+// one workgroup fills a CU, its roles share the SIMDs) or 1 (64 envs, 3 waves, each on a SIMD of
+// its own: for grids that leave most CUs idle, c2's 4,096 envs)
+template <bool TB, bool RAND, bool LDS_TABLE, bool LA = false, bool IOR = false, bool C = false, int PR = 4>
+__global__ void __launch_bounds__(192 * PR) k_rollout1s(Params p, int32_t T, const uint8_t* __restrict__ act,
                                                         uint64_t seed, uint64_t t0, int8_t* __restrict__ rew,
                                                         uint8_t* __restrict__ flg, int4* __restrict__ stats) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1108,7 +1111,7 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
     if constexpr (LDS_TABLE) {
         uint4* lm = reinterpret_cast<uint4*>(smem + kS_Base);
         uint4* lt = lm + NP;
-        for (uint32_t k = threadIdx.x; k < NP; k += kBlock1s) {
+        for (uint32_t k = threadIdx.x; k < NP; k += 192u * PR) {
             lm[k] = p.tab.mrow[k];
             lt[k] = p.tab.trow[k];
         }
@@ -1117,15 +1120,15 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         trow = lt;
     }
     const size_t n = p.n;
-    const uint32_t wg_base = blockIdx.x * 256u;
+    const uint32_t wg_base = blockIdx.x * (64u * PR);
     const int32_t K = T / kTile;
 
-    if (wv >= 8) {                                               // ---- the I/O waves
+    if (wv >= 2u * PR) {                                         // ---- the I/O waves
         // one per SIMD (waves 8-11), each a quarter of the streamed traffic: I/O wave j loads
         // the action tile of pair j and stores rows 8 * (j >> 1) .. + 7 of env half j & 1 of
         // the output tiles (whole 128-B lines).  With one I/O wave for all four pairs its
         // issue load sat on one SIMD (MI355X, c3: 0.468 -> 0.466 ms per launch with four)
-        const uint32_t io = wv - 8u;
+        const uint32_t io = wv - 2u * PR;
         const uint32_t r = lane >> 2, c = (lane & 3u) * 16u;
         const uint32_t pppp = p.pitch * 0x01010101u;
         IoCounters ct;
@@ -1151,8 +1154,10 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
             }
         };
         auto store_tile = [&](int32_t k) {                       // whole 128-B lines, as k_rollout1
-            const uint32_t r8 = lane >> 3, c8 = (lane & 7u) * 16u;
-            const uint32_t h = io >> 1, q = io & 1u;
+            // PR = 4: I/O wave io stores rows 8 * (io >> 1) .. + 7 of env half io & 1 (pairs 2q, 2q+1);
+            // PR = 1: the one I/O wave stores all 16 rows of its pair, 64 B per row
+            const uint32_t r8 = PR == 4 ? lane >> 3 : lane >> 2, c8 = PR == 4 ? (lane & 7u) * 16u : (lane & 3u) * 16u;
+            const uint32_t h = PR == 4 ? io >> 1 : 0u, q = PR == 4 ? io & 1u : 0u;
             const uint32_t row = (uint32_t)((k * kTile) & (kRing - 1)) + h * 8 + r8;
             const uint32_t w = 2 * q + (c8 >> 6);
             const uint8_t* base = smem + w * kS_Pair + row * 64 + (c8 & 63u);
@@ -1185,11 +1190,12 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         // IOR: the byte counters of this lane's 16 envs into the per-env LDS counters (reward sum,
         // done steps, +100 steps), at least every 255 tiles (a lane counts one row per tile)
         auto flush_counts = [&]() {
-            io_flush(ct, reinterpret_cast<int32_t*>(smem + kS_Cnt), (io & 1u) * 128u + (lane & 7u) * 16u);
+            io_flush(ct, reinterpret_cast<int32_t*>(smem + kS_Cnt),
+                     PR == 4 ? (io & 1u) * 128u + (lane & 7u) * 16u : (lane & 3u) * 16u);
         };
         if constexpr (IOR) {
             int32_t* cnt = reinterpret_cast<int32_t*>(smem + kS_Cnt);
-            for (uint32_t x = io * 64u + lane; x < 3u * 256u; x += 256u) cnt[x] = 0;
+            for (uint32_t x = io * 64u + lane; x < 3u * 256u; x += 64u * PR) cnt[x] = 0;
         }
         if (K > 0) load_tile(0);
         __syncthreads();                                         // B_0
@@ -1208,13 +1214,13 @@ __global__ void __launch_bounds__(kBlock1s) k_rollout1s(Params p, int32_t T, con
         return;
     }
 
-    const uint32_t pr = wv & 3u;                                 // the pair's 64 envs
+    const uint32_t pr = wv & (PR - 1u);                          // the pair's 64 envs
     const uint32_t i = wg_base + pr * 64u + lane;
     uint8_t* pb = smem + pr * kS_Pair;
     uint4* fin = reinterpret_cast<uint4*>(smem + kS_Fin) + (IOR ? 1u : 2u) * (pr * 64u + lane);
     // LDS_TABLE = false: this env's trie-row slots (row_slots, sparc_move1.hpp)
     const uint32_t slot_addr = MoveLane1<TB>::lds_addr(smem + kS_Base + (size_t)(pr * 64u + lane) * sizeof(uint4));
-    if (wv < 4) {                                                // ---- move waves
+    if (wv < (uint32_t)PR) {                                     // ---- move waves
         MoveLane1<TB> m;
         uint8_t* col = pb + kS_Stk + lane;
         const uint32_t col_addr = MoveLane1<TB>::lds_addr(col);
@@ -1899,6 +1905,8 @@ struct Ctx {
     // pools past the LDS row budget
     uint8_t* t_trie4 = nullptr;
     uint4* t_trow4 = nullptr;
+    bool mixed_pays = false;   // the 8-B records outgrow an XCD's L2 (sparc_load_puzzles)
+    int mixed_trie = 0;        // SPARC_VARIANT_MIXED_TRIE: 0 when it pays, 1 always, 2 never
     uint4 *t_trow = nullptr, *t_mrow = nullptr;
     // multi-word split kernel (k_rolloutWs): move rows and reset boards; split_w false when the
     // pool does not fit its layout (pitch > 15, LDS, or no trie8)
@@ -2070,6 +2078,7 @@ struct R1Shape {
 };
 
 constexpr uint64_t kFitQueueCap = 1u << 16;   // exact fits past the node cap per audit call (grown)
+constexpr size_t kMixedTrieBytes = (size_t)4 << 20;   // an XCD's L2: past it the mixed trie tables pay
 constexpr uint64_t kFitQueueMax = (uint64_t)1 << 28;   // 6 GB of FitTodo
 
 // the loaded rule table as the kernels take it; queue: push searches past the node cap to the
@@ -2297,6 +2306,7 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
     if (c->t_trow4) HIPCHK(c, hipFree(c->t_trow4));
     c->t_trie4 = nullptr;
     c->t_trow4 = nullptr;
+    c->mixed_pays = false;
     if (c->t_trow) HIPCHK(c, hipFree(c->t_trow));
     if (c->t_mrow) HIPCHK(c, hipFree(c->t_mrow));
     if (c->t_mroww) HIPCHK(c, hipFree(c->t_mroww));
@@ -2463,7 +2473,11 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
         // mixed tables (TrieLaneT<true>): a trie of at most 127 nodes as 4-B records (each 16-bit
         // field of trie8 as an 8-bit one, index | terminal << 7, 0xFF none), a larger one as its
         // 8-B records; each puzzle's records start on a 128-B line, the base is a byte offset, and
-        // bit 13 of the row's w marks a compact puzzle (root S then 0x80 / 0x100)
+        // bit 13 of the row's w marks a compact puzzle (root S then 0x80 / 0x100).  Used when the
+        // 8-B records outgrow an XCD's 4 MB L2: below that the per-lane format costs the trie chain
+        // more than the misses it saves (MI355X, c3: 4,096 puzzles, 2 MB of records, +5 %; 16,384
+        // puzzles, 8.4 MB, -7.4 %; profiles/r06/ab_bigpool); SPARC_VARIANT_MIXED_TRIE overrides
+        c->mixed_pays = nn8 * sizeof(uint2) > kMixedTrieBytes;
         if (W == 1) {
             std::vector<size_t> bo(P, 0);
             size_t nb = 0;
@@ -2689,7 +2703,7 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
             const size_t shm_s = kS_Base + (lds_s ? sbytes : kS_SlotBytes);
             // past the row budget the mixed tables (tries of at most 127 nodes in 4-B records:
             // twice the nodes per L2 line; sparc_trie.hpp TrieLaneT<true>)
-            const bool compact = !lds_s && c->t_trie4;
+            const bool compact = !lds_s && c->t_trie4 && (c->mixed_trie == 1 || (c->mixed_trie == 0 && c->mixed_pays));
             Params ps = p;
             if (compact) {
                 ps.tab.trie8 = reinterpret_cast<const uint2*>(c->t_trie4);
@@ -2699,6 +2713,14 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
                 if (shm_s > 64 * 1024 && (lds_rc = allow_big_lds(c, reinterpret_cast<const void*>(kern)))) return;
                 kern<<<dim3((unsigned)blocks), kBlock1s, shm_s, c->stream>>>(ps, T16, a, seed, t0, d_rew, d_flags, st);
             };
+            // one wave pair (and its I/O wave) per workgroup: 4x the workgroups, each role on a SIMD
+            // of its own
+            auto launch_s1 = [&](auto kern, const uint8_t* a) {
+                if (shm_s > 64 * 1024 && (lds_rc = allow_big_lds(c, reinterpret_cast<const void*>(kern)))) return;
+                kern<<<dim3((unsigned)(4 * blocks)), kBlock1s / 4, shm_s, c->stream>>>(ps, T16, a, seed, t0, d_rew, d_flags,
+                                                                                     st);
+            };
+            (void)launch_s1;
             // IOR (next-step autoreset): the I/O waves derive the reward codes and counters from
             // the trie wave's class bytes (io_codes4), which takes them off the trie wave's chain
             auto go_s = [&](auto tb, auto ior) {
@@ -3450,6 +3472,10 @@ int sparc_set_variant(void* ctx, int32_t which, int32_t value) {
         case SPARC_VARIANT_OBS_INLINE:
             if (value != 0 && value != 1) break;
             c->obs_inline = value == 1;
+            return SPARC_OK;
+        case SPARC_VARIANT_MIXED_TRIE:
+            if (value < 0 || value > 2) break;
+            c->mixed_trie = value;
             return SPARC_OK;
         default:
             return fail(c, SPARC_E_INVALID, "unknown variant");

@@ -70,16 +70,10 @@ struct MoveLaneW {
     // the window at e and the legal mask of the current state (1024-1051); traceback: path[-2]
     // (the reverse of the last move, rl) is legal although visited when len >= 3, or len == 2
     // and the start is open (bk bias, as Env<1>)
-    __device__ __forceinline__ uint64_t window_at(uint32_t x) const {
-        const uint32_t k = x >> 5;
-        const uint64_t pr = ((uint64_t)dw(k + 1u) << 32) | dw(k);
-        return pr >> (x & 31u);
-    }
     __device__ __forceinline__ void read_window(const SplitGeom& g) {
-        w = window_at(e);
-        set_legal(g);
-    }
-    __device__ __forceinline__ void set_legal(const SplitGeom& g) {
+        const uint32_t k = e >> 5;
+        const uint64_t pr = ((uint64_t)dw(k + 1u) << 32) | dw(k);
+        w = pr >> (e & 31u);
         const uint32_t lo = (uint32_t)w;
         const uint32_t ud = __builtin_amdgcn_ubfe(lo, g.P2 - 2u, 4u);
         uint32_t m = (ud & 10u) | ((lo << 2) & 4u) | ((uint32_t)(w >> (2u * g.P2)) & 1u);
@@ -128,27 +122,17 @@ struct MoveLaneW {
             // would wait for them
             asm volatile("" ::"v"(e), "v"(tgt), "v"(bk) : "memory");
             prefetch_next(p, g, mrow, boards);   // waited for at the next reset
-            read_window(g);                      // the fresh board's window (phase_move keeps it)
         }
     }
 
     // one step's move part (1131-1199): legality, move or traceback pop, path, terminated /
-    // truncated; returns the flag byte.  The window of the next state is read SPECULATIVELY at
-    // the start of the step: a step moves nowhere or to ec = e + pos - P (a forward move and a
-    // traceback pop both move in the action's direction), so the window at ec is read before this
-    // step's toggle and patched in registers (the toggled point sits at window bit P after a
-    // forward move, 2P - pos after a pop); the LDS read's latency is then off the step's chain
+    // truncated; returns the flag byte
     __device__ __forceinline__ uint32_t phase_move(const Params& p, const SplitGeom& g, uint32_t a) {
         const uint32_t P = g.P2;
         step = __builtin_elementwise_add_sat(step, 1);                              // 1132
         const bool trunc0 = step >= p.max_steps;                                    // 1134
-        const uint32_t ac = a < 4u ? a : 4u;
-        const uint32_t moved = (legal >> ac) & (rs ^ 1u) & 1u;                      // 1137
-        // the target's window bit; P (the agent's own point) for an illegal action, so ec = e
-        const uint32_t pos = __builtin_amdgcn_perm(P * 0x01010101u, g.nbr_pos, ac | 0x0C0C0C00u);
-        const uint32_t ec = e + pos - P;
-        const uint64_t wc = window_at((int32_t)ec < 0 ? 0u : ec);   // (used only if the move is legal)
-        asm volatile("" ::: "memory");   // the read stays ahead of this step's toggle
+        const uint32_t moved = (legal >> (a < 4u ? a : 4u)) & (rs ^ 1u) & 1u;       // 1137
+        const uint32_t pos = __builtin_amdgcn_ubfe(g.nbr_pos, a << 3, 8u);
         // the only legal move onto a non-free point is the traceback pop (1141-1166)
         const uint32_t pop = TB ? moved & ~(uint32_t)(w >> pos) & 1u : 0u;
         const uint32_t fwd = moved ^ pop;                                            // 1167-1188
@@ -162,9 +146,8 @@ struct MoveLaneW {
             rl = fwd ? ar : (pop ? pnr : rl);
         }
         len = len + fwd - pop;
-        e = moved ? ec : e;
-        w = moved ? wc ^ (1ull << (fwd ? P : 2u * P - pos)) : w;
-        set_legal(g);
+        e = (uint32_t)((int32_t)e + __mul24((int32_t)moved, (int32_t)pos - (int32_t)P));
+        read_window(g);
         const uint32_t live = rs ^ 1u;                                               // 0 on a reset step
         const uint32_t term = e == tgt ? live : 0u;                                  // 1192
         const uint32_t trunc = (trunc0 | (legal == 0)) ? live ^ term : 0u;          // 1195-1199

@@ -121,19 +121,26 @@ def pool2048():
 
 @pytest.mark.parametrize("max_steps", [1, 2, 3, 7, 2000])
 @pytest.mark.parametrize("tb", [True, False])
-def test_slot_fallback_short_episodes_vs_oracle(on_gpu, pool2048, max_steps, tb):
+@pytest.mark.parametrize("mixed", [0, 1])
+def test_slot_fallback_short_episodes_vs_oracle(on_gpu, pool2048, max_steps, tb, mixed):
     """Autoresets every 2-8 steps: two resets of an env within two tiles make the move wave
     write its spare slot and the trie wave read the row from the L2 (the slot rule); launches of
     64 + 48 + 37 steps (the last one's 5-step tail through k_rollout1), the state round-tripping
-    through HBM: reward codes, flags, stats and state against the C oracle."""
+    through HBM: reward codes, flags, stats and state against the C oracle.  mixed = 1 forces the
+    mixed trie tables (SPARC_VARIANT_MIXED_TRIE: 4-B records for tries of <= 127 nodes, 8-B ones
+    for the larger tries of this pool; by default only pools past 4 MB of records take them)."""
     from sparc_gym_amd import SPaRCVecEnv
     proc, table = pool2048
     assert len(proc) > LDS_ROW_LIMIT and table.words == 1
+    if mixed:
+        cnt = table.info[:, 3] & 0xFFFF
+        assert (cnt > 127).any() and (cnt <= 127).any()   # both record formats in one pool
     n = 4096
     rng = np.random.default_rng(max_steps + 100 * tb)
     pids = rng.integers(len(proc), size=n)
     v = SPaRCVecEnv(n, processed=proc, table=table, traceback=tb, max_steps=max_steps, autoreset="next_step",
                     observation="compact")
+    v.core.set_variant(v.core.VARIANT_MIXED_TRIE, 1 if mixed else 2)
     v.reset(options={"puzzle_index": pids})
     o = COracle(_oracle_pool(proc), n, tb, max_steps, autoreset=1)
     o.reset(pids)

@@ -376,5 +376,8 @@ def test_c4_bench_launch_shape_every_env(on_gpu, config):
     ost, so = ora.final()
     assert np.array_equal(stats.cpu().numpy(), ost)
     _state_equal(v.state(), so, table)
+    # the workload exercised what the bench measures: episodes end at the target and autoresets
+    # follow (truncation needs max_steps 2,000 steps or a dead end, which traceback rules out: c4's
+    # 100 steps have none)
     f_all = flg.cpu().numpy().reshape(-1, n)
-    assert ((f_all & 1) != 0).sum() > 0 and ((f_all & 2) != 0).sum() > 0 and ((f_all & 64) != 0).sum() > 0
+    assert ((f_all & 1) != 0).sum() > 0 and ((f_all & 64) != 0).sum() > 0

@@ -98,13 +98,13 @@ VARIANTS = {
     "prio21": [("sparc_kernels.hip", """        __builtin_amdgcn_s_setprio(1);
         static_assert(!(C && LA),""", """        __builtin_amdgcn_s_setprio(2);
         static_assert(!(C && LA),"""),
-               ("sparc_kernels.hip", """    if (wv < 4) {                                                // ---- move waves
-        MoveLane1<TB> m;""", """    if (wv < 4) {                                                // ---- move waves
+               ("sparc_kernels.hip", """    if (wv < (uint32_t)PR) {                                     // ---- move waves
+        MoveLane1<TB> m;""", """    if (wv < (uint32_t)PR) {                                     // ---- move waves
         __builtin_amdgcn_s_setprio(1);
         MoveLane1<TB> m;""")],
     # the same with the move and trie waves at 1 (only the I/O waves yield)
-    "prio11": [("sparc_kernels.hip", """    if (wv < 4) {                                                // ---- move waves
-        MoveLane1<TB> m;""", """    if (wv < 4) {                                                // ---- move waves
+    "prio11": [("sparc_kernels.hip", """    if (wv < (uint32_t)PR) {                                     // ---- move waves
+        MoveLane1<TB> m;""", """    if (wv < (uint32_t)PR) {                                     // ---- move waves
         __builtin_amdgcn_s_setprio(1);
         MoveLane1<TB> m;""")],
     # the split tables without the 128-B line alignment of each puzzle's trie records
@@ -144,11 +144,10 @@ VARIANTS = {
         pending = pu != 0u;"""),
                  ("sparc_move1.hpp", "        return ((uint32_t)dl << 30) | ((at_tgt | rs) ? kHwTgt : 0u) | (pending ? kHwDone : 0u) | lw;",
                   "        return ((uint32_t)dl << 30) | ((at | rsu) << 24) | (pu << 25) | lw;")],
-    # k_rollout1s on the mixed trie tables (compact 4-B records) although the rows fit LDS
-    "mixed": [("sparc_kernels.hip", """                    else if (lds_s) launch_s(k_rollout1s<TB, false, true, false, IOR>, d_act);""",
-               """                    else if (lds_s) launch_s(k_rollout1s<TB, false, true, false, IOR, true>, d_act);"""),
-              ("sparc_kernels.hip", """            const bool compact = !lds_s && c->t_trie4;""",
-               """            const bool compact = c->t_trie4 && !(lds_s && blocks <= 64);""")],
+    # k_rollout1s on grids of at most 64 256-env workgroups (c2): one wave pair + its I/O wave per
+    # 64-env workgroup (PR = 1), so the move, trie and I/O waves each get a SIMD of their own
+    "pr1": [("sparc_kernels.hip", "if (lds_s && blocks <= 64) launch_s(k_rollout1s<TB, false, true, true, IOR>, d_act);",
+             "if (lds_s && blocks <= 64) launch_s1(k_rollout1s<TB, false, true, true, IOR, false, 1>, d_act);")],
     # k_rollout1r with s_memtime stamps (timing only: the stats buffer receives, per wave, role |
     # total | barrier-wait | audit cycles at index N/2 + block * 16 + wave; tools/diag_r1r.py)
     "stamps": [
