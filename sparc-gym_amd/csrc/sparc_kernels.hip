@@ -1387,15 +1387,20 @@ struct R1Geom {
     static constexpr size_t kBits = kFlg + 3 * RT * kEnvs;                 // [2][RT][kEnvs] u16 rule bits
     static constexpr size_t kAct = kBits + 2 * RT * kEnvs * 2;             // [G][RT][64] actions of the tile
     static constexpr size_t kStk = kAct + G * RT * 64;                     // [G][64 moves][64] move stacks
-    static constexpr size_t kBase = kStk + (size_t)G * 64 * 64;            // then the W = 1 puzzle rows
+    static constexpr size_t kSimple = kStk + (size_t)G * 64 * 64;          // [512] ring_simple (INC audits)
+    static constexpr size_t kBase = kSimple + 512;                         // then the W = 1 puzzle rows
 };
 constexpr uint32_t kRingShift = 57;
 
+// INC: incremental audits (RegionSet1, sparc_rules.hpp): audit wave q takes the steps of the
+// q-th block of RT / A consecutive steps of each tile in order, keeping the env's regions from
+// one step to the next (A = 1: across tiles too, so a full flood only after a reset or a puzzle
+// change; A > 1: one full flood at the start of each block).
 // amdgpu_waves_per_eu(6): two 12-wave workgroups per CU (3 waves per SIMD each).  Left to itself
 // the compiler takes 92 VGPRs (5 waves per SIMD, one workgroup per CU: 0.145 ms per 50-step launch
 // against 0.121 ms with 80 VGPRs and 24 B of scratch touched once per tile).
-template <bool TB, bool RAND, bool LDS_TABLE, int G, int A, int RT>
-__global__ void __launch_bounds__(64 * G * (1 + A)) __attribute__((amdgpu_waves_per_eu(6)))
+template <bool TB, bool RAND, bool LDS_TABLE, int G, int A, int RT, bool INC = false, int WPE = 6>
+__global__ void __launch_bounds__(64 * G * (1 + A)) __attribute__((amdgpu_waves_per_eu(WPE)))
     k_rollout1r(Params p, int32_t T, const uint8_t* __restrict__ act, uint64_t seed, uint64_t t0,
                 int8_t* __restrict__ rew, uint8_t* __restrict__ flg, int4* __restrict__ stats, uint32_t tiled,
                 RulesTab rt, uint16_t* __restrict__ bits) {
@@ -1419,6 +1424,9 @@ __global__ void __launch_bounds__(64 * G * (1 + A)) __attribute__((amdgpu_waves_
     auto at = [](uint32_t b, int32_t j, uint32_t c) { return (b * (uint32_t)RT + (uint32_t)j) * E + c; };
     auto tile_cnt = [&](int32_t k) { return T - k * RT < RT ? T - k * RT : RT; };
     PuzzleSrc<1> src{p.tab.info, p.tab.root, p.tab.open, p.tab.init, p.tab.row1};
+    if constexpr (INC) {   // read by the audit waves after B_1
+        for (uint32_t k = threadIdx.x; k < 512u; k += Geo::kBlock) smem[Geo::kSimple + k] = (uint8_t)ring_simple(k);
+    }
     if constexpr (LDS_TABLE) {
         const uint32_t P = p.tab.num_puzzles;
         uint4* lrow1 = reinterpret_cast<uint4*>(smem + Geo::kBase);
@@ -1574,11 +1582,36 @@ __global__ void __launch_bounds__(64 * G * (1 + A)) __attribute__((amdgpu_waves_
     }
 
     // ---- audit waves
-    const uint32_t q = wv / (uint32_t)G - 1u;                    // audits the steps t % A == q
+    const uint32_t q = wv / (uint32_t)G - 1u;                    // audits the steps t % A == q (INC: block q)
     PuzzleRules<1> pr;
     pr.q = 0xFFFFFFFFu;
     __syncthreads();                                             // B_0
     __syncthreads();                                             // B_1 (interval 0: no tile yet)
+    if constexpr (INC) {
+        constexpr int32_t BL = RT / A;                           // steps per block
+        const uint8_t* simple = smem + Geo::kSimple;
+        RegionSet1 rs;
+        for (int32_t k = 1; k <= K; ++k) {
+            const int32_t kt = k - 1, cnt = tile_cnt(kt);
+            const uint32_t b = (uint32_t)kt & 1u;
+            const int32_t j0 = (int32_t)q * BL, j1 = j0 + BL < cnt ? j0 + BL : cnt;
+            if (A > 1) rs.q = 0xFFFFFFFFu;                       // the block's first step: a full flood
+#pragma unroll 1
+            for (int32_t j = j0; j < j1; ++j) {
+                const uint64_t w = ring[at(b, j, col)];
+                const uint32_t pid = rpid[at(b, j, col)];
+                uint32_t out = 0;
+                if (active) {
+                    if (pr.q != pid) pr = puzzle_rules<1>(p, rt, pid);
+                    const uint32_t ab = (uint32_t)(w >> kRingShift) & 63u;
+                    out = rs.audit(p, rt, pr, w & ((1ull << kRingShift) - 1ull), ab == pr.tbit, simple);
+                }
+                tbt[at(b, j, col)] = (uint16_t)out;
+            }
+            __syncthreads();                                     // B_{k+1}
+        }
+        return;
+    }
     for (int32_t k = 1; k <= K; ++k) {
         const int32_t kt = k - 1, cnt = tile_cnt(kt);
         const uint32_t b = (uint32_t)kt & 1u;
@@ -1935,7 +1968,7 @@ struct Ctx {
     // kernel variants with identical results, set only by sparc_set_variant (A/B runs, tests)
     bool rules_generic = false;   // rule rollouts on k_rollout<..., RULES>
     bool io_codes_off = false;    // k_rollout1s / k_rolloutWs keep the reward codes on the trie wave
-    int r1r_shape = 0;            // k_rollout1r's <G, A, RT> (0: <2, 5, 10>; 1, 2: A/B, tests)
+    int r1r_shape = 0;            // k_rollout1r's <G, A, RT> (0: <2, 5, 10>; 1-4: A/B, tests)
     bool obs_inline = false;      // 'new'-plane rollouts on k_rollout<..., OBS> instead of k_rollout_obsw
     // exact-fit searches past the GPU's node cap (sparc_set_fit_cap) are finished on the host
     // from these copies of the rule table (sparc_rules.hpp exact_fit, the same code)
@@ -2072,9 +2105,10 @@ int launch_check(Ctx* c) {
     return SPARC_OK;
 }
 
-template <int G_, int A_, int RT_>
+template <int G_, int A_, int RT_, bool INC_ = false, int WPE_ = 6>
 struct R1Shape {
-    static constexpr int G = G_, A = A_, RT = RT_;
+    static constexpr int G = G_, A = A_, RT = RT_, WPE = WPE_;
+    static constexpr bool INC = INC_;
 };
 
 constexpr uint64_t kFitQueueCap = 1u << 16;   // exact fits past the node cap per audit call (grown)
@@ -2713,21 +2747,22 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
                 if (shm_s > 64 * 1024 && (lds_rc = allow_big_lds(c, reinterpret_cast<const void*>(kern)))) return;
                 kern<<<dim3((unsigned)blocks), kBlock1s, shm_s, c->stream>>>(ps, T16, a, seed, t0, d_rew, d_flags, st);
             };
-            // one wave pair (and its I/O wave) per workgroup: 4x the workgroups, each role on a SIMD
-            // of its own
+            // one wave pair (and its I/O wave) per workgroup (k_rollout1s<..., PR = 1>): 4x the
+            // workgroups, each role on a SIMD of its own, for grids of at most 64 256-env
+            // workgroups (MI355X, c2 at 4,096 envs: 0.2811-0.2817 -> 0.2744-0.2750 ms per 2,000-step
+            // launch, profiles/r06/ab_c2_pr1)
             auto launch_s1 = [&](auto kern, const uint8_t* a) {
                 if (shm_s > 64 * 1024 && (lds_rc = allow_big_lds(c, reinterpret_cast<const void*>(kern)))) return;
                 kern<<<dim3((unsigned)(4 * blocks)), kBlock1s / 4, shm_s, c->stream>>>(ps, T16, a, seed, t0, d_rew, d_flags,
                                                                                      st);
             };
-            (void)launch_s1;
             // IOR (next-step autoreset): the I/O waves derive the reward codes and counters from
             // the trie wave's class bytes (io_codes4), which takes them off the trie wave's chain
             auto go_s = [&](auto tb, auto ior) {
                 constexpr bool TB = decltype(tb)::value, IOR = decltype(ior)::value;
                 if (d_act) {
                     // look-ahead trie gathers on grids of at most 64 workgroups (sparc_trie.hpp)
-                    if (lds_s && blocks <= 64) launch_s(k_rollout1s<TB, false, true, true, IOR>, d_act);
+                    if (lds_s && blocks <= 64) launch_s1(k_rollout1s<TB, false, true, true, IOR, false, 1>, d_act);
                     else if (lds_s) launch_s(k_rollout1s<TB, false, true, false, IOR>, d_act);
                     else if (compact) launch_s(k_rollout1s<TB, false, false, false, IOR, true>, d_act);
                     else launch_s(k_rollout1s<TB, false, false, false, IOR>, d_act);
@@ -2781,7 +2816,8 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
         // audit waves (k_rollout1r; shape <G, A, RT> = c->r1r_shape)
         auto go_shape = [&](auto geo_c) {
             using Geo = decltype(geo_c);
-            constexpr int G = Geo::G, A = Geo::A, RT = Geo::RT;
+            constexpr int G = Geo::G, A = Geo::A, RT = Geo::RT, WPE = Geo::WPE;
+            constexpr bool INC = Geo::INC;
             using GG = R1Geom<G, A, RT>;
             const size_t blocks = (c->n + GG::kEnvs - 1) / GG::kEnvs;
             const size_t tbytes = table_lds_bytes<1>(c->num_puzzles);
@@ -2795,11 +2831,11 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
             auto go = [&](auto tb) {
                 constexpr bool TB = decltype(tb)::value;
                 if (d_act) {
-                    if (lds_table) launch(k_rollout1r<TB, false, true, G, A, RT>, d_act);
-                    else launch(k_rollout1r<TB, false, false, G, A, RT>, d_act);
+                    if (lds_table) launch(k_rollout1r<TB, false, true, G, A, RT, INC, WPE>, d_act);
+                    else launch(k_rollout1r<TB, false, false, G, A, RT, INC, WPE>, d_act);
                 } else {
-                    if (lds_table) launch(k_rollout1r<TB, true, true, G, A, RT>, nullptr);
-                    else launch(k_rollout1r<TB, true, false, G, A, RT>, nullptr);
+                    if (lds_table) launch(k_rollout1r<TB, true, true, G, A, RT, INC, WPE>, nullptr);
+                    else launch(k_rollout1r<TB, true, false, G, A, RT, INC, WPE>, nullptr);
                 }
             };
             if (c->cfg.traceback) go(std::true_type{});
@@ -2812,6 +2848,11 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
         switch (c->r1r_shape) {
             case 1: go_shape(R1Shape<4, 3, 12>{}); break;
             case 2: go_shape(R1Shape<2, 4, 12>{}); break;
+            // incremental audits (INC, RegionSet1): slower in lock step, kept for A/B and tests —
+            // c3r 2,000-step launches 7.6 ms (<4, 1, 4>) and 6.1-6.3 ms (<2, 3, 15>) against 3.92-3.99
+            // (<2, 1, 8> 9.2, <2, 2, 16> 7.8; profiles/r06/ab_c3r_inc)
+            case 3: go_shape(R1Shape<4, 1, 4, true, 4>{}); break;
+            case 4: go_shape(R1Shape<2, 3, 15, true, 4>{}); break;
             default: go_shape(R1Shape<2, 5, 10>{}); break;
         }
         if (lds_rc) return lds_rc;
@@ -3466,7 +3507,7 @@ int sparc_set_variant(void* ctx, int32_t which, int32_t value) {
             c->rules_generic = value == 1;
             return SPARC_OK;
         case SPARC_VARIANT_R1R_SHAPE:
-            if (value < 0 || value > 2) break;
+            if (value < 0 || value > 4) break;
             c->r1r_shape = value;
             return SPARC_OK;
         case SPARC_VARIANT_OBS_INLINE:

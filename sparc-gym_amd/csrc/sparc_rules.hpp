@@ -575,6 +575,19 @@ __device__ __forceinline__ uint32_t audit_path(uint32_t P, const PuzzleRules<W>&
     return (uint32_t)reached | 2u | ((uint32_t)gap_ok << 2) | ((uint32_t)dot_ok << 3) | ((uint32_t)tri_ok << 6);
 }
 
+// One dilation of R (within a) on the padded one-word board: a y step off the lattice lands on a
+// blocked bit, so each lattice row's runs of allowed bits end below a zero.  Toward +y the whole
+// run above each bit of R fills in one add: the carry from R ripples up through the run (the
+// allowed bits it clears, plus the seeds, are the fill).  -y and +-x stay one step per iteration.
+// Flood iterations per 64-env wave-step (c3 pool, random walks, regions in lock step): one step
+// each way 39.9, +y runs 34.4.  The -y runs by the same add on the bit-reversed board (two more
+// 64-bit adds and four bit reversals per iteration) cost more than the iterations they save:
+// MI355X, c3r 2,000-step launches 3.956 -> 4.11-4.14 ms (profiles/r06/ab_c3r_inc).
+__device__ __forceinline__ uint64_t dilate_w1(uint64_t r, uint64_t a, uint32_t P) {
+    const uint64_t up = (((a + r) ^ a) & a) | r;
+    return (up | (r >> 1) | (r << P) | (r >> P)) & a;
+}
+
 // vis: path points; reached: the agent is on the target (_rule_reached_target 487-495); pr: the
 // env's puzzle (puzzle_rules).  region_out (may be null): region id per bit.  memo (FitMemo, or
 // NoMemo): exact-fit answers carried between calls of one lane (puzzles without a region-code
@@ -622,17 +635,9 @@ __device__ RuleOut<W> audit_r(const Params& p, const RulesTab& rt, const PuzzleR
         R.set(remaining.lowest());
         while (true) {                                           // flood fill (BFS 431-452)
             BB<W> N;
-            if constexpr (W == 1) {
-                // the padded one-word geometry: a y step off the lattice lands on a blocked bit,
-                // so each lattice row's runs of allowed bits end below a zero.  Toward +y the
-                // whole run above each bit of R (R within allowed) fills in one add: the carry
-                // from R ripples up through the run (the allowed bits it clears, plus the seeds,
-                // are the fill).  -y and +-x stay one step per iteration.  Flood iterations per
-                // 64-env wave-step (c3 pool, random walks, regions run in lock step): 39.9 -> 34.4
-                const uint64_t a = allowed.w[0], r = R.w[0];
-                const uint64_t up = (((a + r) ^ a) & a) | r;
-                N.w[0] = up | (r >> 1) | (r << P) | (r >> P);
-            } else
+            if constexpr (W == 1)
+                N.w[0] = dilate_w1(R.w[0], allowed.w[0], P);   // whole +y runs per iteration
+            else
                 N = R | (R.shl(1) & nfirst) | (R.shr(1) & nlast) | R.shl(P) | R.shr(P);
             N = N & allowed;
             if (N == R) break;
@@ -675,6 +680,201 @@ __device__ RuleOut<W> audit_r(const Params& p, const RulesTab& rt, const PuzzleR
     bits |= (uint32_t)exhausted << 9;
     return RuleOut<W>{bits, fit_ok};
 }
+
+// ---------------------------------------------------------------- incremental regions (W = 1)
+// A rule rollout audits every step of an env, and consecutive steps differ by ONE path point
+// (a forward move adds it, a traceback pop removes it); the regions (_compute_regions 422-454)
+// are a function of the allowed set alone, so they follow incrementally:
+//  * a point p leaving the allowed set (a move onto it): only the region holding it changes.  When
+//    the allowed 4-neighbours of p lie in one run of allowed points around p (its 8-ring, each
+//    ring point 4-adjacent to the next: kRingSimple below), any path through p detours through
+//    the ring, so the region just loses p (its cells, and so its check code, are unchanged); else
+//    the region is flooded again from its cells (it may split; pieces without a cell are no
+//    region);
+//  * a point p joining the allowed set (a pop): the regions of its allowed 4-neighbours merge
+//    with p (and with any isolated corner point next to it: every allowed edge point touches a
+//    cell, so the only allowed points outside every region are corners whose four edge points are
+//    blocked).  Merging two or more regions makes a new cell mask: one table lookup.
+// The rule bits need the regions only as a set (squares, stars and poly / ylop are per-region
+// codes, AND-ed), so the slots carry no order.  A reset, a puzzle change or any other change of
+// more than one point rebuilds the set by the full flood.
+constexpr int kRegions1 = 9;   // cells of a one-word board (7 x 7 lattice: 3 x 3)
+
+// the 3 x 3 neighbourhood of p as a 9-bit index, bit 3 (dx + 1) + (dy + 1) = point (x + dx, y + dy)
+// allowed (a: allowed board, bit x * P + y; needs p + P + 1 < 64 + P + 1 and the board below bit
+// 63 - P - 1, host-checked)
+__device__ __forceinline__ uint32_t ring_index(uint64_t a, uint32_t p, uint32_t P) {
+    const uint64_t b = (a << (P + 1u)) >> p;
+    return (uint32_t)(b & 7u) | ((uint32_t)((b >> P) & 7u) << 3) | ((uint32_t)((b >> (2u * P)) & 7u) << 6);
+}
+// 1 when the allowed 4-neighbours of the centre lie in at most one run of the ring (index as
+// ring_index; the centre bit ignored)
+__host__ __device__ inline uint32_t ring_simple(uint32_t idx) {
+    const int order[8] = {3, 6, 7, 8, 5, 2, 1, 0};   // ring: (0,-1) (1,-1) (1,0) (1,1) (0,1) (-1,1) (-1,0) (-1,-1)
+    int first_gap = -1;
+    for (int k = 0; k < 8; ++k)
+        if (!((idx >> order[k]) & 1u)) { first_gap = k; break; }
+    if (first_gap < 0) return 1u;                     // the whole ring allowed: one run
+    int runs = 0;
+    bool in = false, has4 = false;
+    for (int k = 1; k <= 8; ++k) {                    // walk the ring from just after a gap
+        const int pos = (first_gap + k) & 7;
+        const bool on = (idx >> order[pos]) & 1u;
+        if (on) {
+            if (!in) { in = true; has4 = false; }
+            has4 |= (pos & 1) == 0;                   // even ring positions are the 4-neighbours
+        } else if (in) {
+            in = false;
+            runs += has4 ? 1 : 0;
+        }
+    }
+    if (in) runs += has4 ? 1 : 0;
+    return runs <= 1 ? 1u : 0u;
+}
+
+// Slot k holds region k's points (bits below kRingShift = 57: every board of a rule rollout) and,
+// in bits 60-63, its region code; 0: a free slot.
+constexpr uint32_t kRsCodeShift = 60;
+constexpr uint64_t kRsPoints = (1ull << kRsCodeShift) - 1ull;
+struct RegionSet1 {
+    uint64_t m[kRegions1];      // region points | code << kRsCodeShift
+    uint32_t agg = 0;           // kRcSq | kRcStar | poly_ok << 2 | exhausted << 3 over the regions
+    uint64_t vis = 0;           // the path board they describe
+    uint32_t q = 0xFFFFFFFFu;   // and its puzzle (none yet)
+
+    __device__ __forceinline__ static uint64_t flood(uint64_t seed, uint64_t a, uint32_t P) {
+        uint64_t r = seed;
+        while (true) {   // as audit_r's W = 1 flood
+            const uint64_t nx = dilate_w1(r, a, P);
+            if (nx == r) return r;
+            r = nx;
+        }
+    }
+    // R's points | its region code << kRsCodeShift
+    __device__ __forceinline__ static uint64_t with_code(const RulesTab& rt, const PuzzleRules<1>& pr, uint64_t R,
+                                                         uint32_t P) {
+        const uint64_t rc = R & pr.pl[kB_CELLS].w[0];
+        BB<1> Rc;
+        Rc.w[0] = rc;
+        const uint32_t m = (uint32_t)(P == 8u ? cell_mask_p8(pr.fin, rc) : cell_mask<1>(pr.fin, Rc, P));
+        const uint32_t code = (rt.reg_tab[(pr.fo + m) >> 3] >> ((m & 7u) * 4u)) & 15u;
+        return R | ((uint64_t)code << kRsCodeShift);
+    }
+    __device__ __forceinline__ void set_agg() {
+        uint32_t sq = kRcSq, st = kRcStar, po = 1u, ex = 0u;
+#pragma unroll
+        for (int k = 0; k < kRegions1; ++k) {
+            const bool live = m[k] != 0ull;
+            const uint32_t code = (uint32_t)(m[k] >> kRsCodeShift);
+            sq &= live ? code : kRcSq;
+            st &= live ? code : kRcStar;
+            po &= (live && (code >> kRcPolyShift) == 2u) ? 0u : 1u;
+            ex |= (live && (code >> kRcPolyShift) == 3u) ? 1u : 0u;
+        }
+        agg = (sq & kRcSq) | (st & kRcStar) | (po << 2) | (ex << 3);
+    }
+    // every region from scratch (a reset, another puzzle, a change of more than one point)
+    __device__ void rebuild(const RulesTab& rt, const PuzzleRules<1>& pr, uint64_t a, uint32_t P) {
+        uint64_t remaining = pr.pl[kB_CELLS].w[0];
+#pragma unroll
+        for (int k = 0; k < kRegions1; ++k) {
+            m[k] = 0ull;
+            if (remaining) {
+                const uint64_t R = flood(remaining & (~remaining + 1ull), a, P);
+                m[k] = with_code(rt, pr, R, P);
+                remaining &= ~R;
+            }
+        }
+        set_agg();
+    }
+    // p left the allowed set (a = the allowed board without it)
+    __device__ void remove(const RulesTab& rt, const PuzzleRules<1>& pr, uint64_t a, uint32_t p, uint32_t P,
+                           const uint8_t* simple) {
+        const uint64_t bit = 1ull << p;
+        uint64_t hit = 0ull;
+#pragma unroll
+        for (int k = 0; k < kRegions1; ++k) hit |= m[k] & bit;
+        if (!hit) return;                                         // an isolated corner: no region
+        if (simple[ring_index(a, p, P)]) {                        // no split: the region loses p
+#pragma unroll
+            for (int k = 0; k < kRegions1; ++k) m[k] &= ~bit;
+            return;
+        }
+        uint64_t R = 0ull;
+#pragma unroll
+        for (int k = 0; k < kRegions1; ++k) {
+            const bool h = (m[k] & bit) != 0ull;
+            R = h ? m[k] & kRsPoints & ~bit : R;
+            m[k] = h ? 0ull : m[k];
+        }
+        uint64_t rest = R & pr.pl[kB_CELLS].w[0];
+        while (rest) {                                            // the pieces that hold cells
+            const uint64_t piece = flood(rest & (~rest + 1ull), a, P);
+            const uint64_t e = with_code(rt, pr, piece, P);
+            bool placed = false;
+#pragma unroll
+            for (int k = 0; k < kRegions1; ++k) {
+                const bool here = !placed && m[k] == 0ull;
+                m[k] = here ? e : m[k];
+                placed |= here;
+            }
+            rest &= ~piece;
+        }
+        set_agg();
+    }
+    // p joined the allowed set (a = the allowed board with it)
+    __device__ void add(const RulesTab& rt, const PuzzleRules<1>& pr, uint64_t a, uint32_t p, uint32_t P) {
+        const uint64_t bit = 1ull << p;
+        if (!(a & bit)) return;                                   // a gap left the path: no change
+        const uint64_t nb = (((bit << 1) | (bit >> 1) | (bit << P) | (bit >> P)) & a);
+        uint64_t all = 0ull, merged = 0ull, keep = 0ull;
+        uint32_t hits = 0;
+#pragma unroll
+        for (int k = 0; k < kRegions1; ++k) {
+            all |= m[k];
+            const bool h = (m[k] & nb) != 0ull;
+            keep = (h && hits == 0u) ? m[k] : keep;               // the first region hit (its code)
+            merged |= h ? m[k] : 0ull;
+            hits += h ? 1u : 0u;
+        }
+        if (hits == 0u) return;                                   // p and isolated corners: no cell
+        // p, and the isolated corners beside it
+        merged = (merged & kRsPoints) | bit | (nb & ~all);
+        uint64_t e = merged | (keep & ~kRsPoints);
+        if (hits > 1u) e = with_code(rt, pr, merged, P);          // a new cell set: its code
+        bool placed = false;
+#pragma unroll
+        for (int k = 0; k < kRegions1; ++k) {
+            const bool h = (m[k] & nb) != 0ull;
+            m[k] = h ? (placed ? 0ull : e) : m[k];
+            placed |= h;
+        }
+        if (hits > 1u) set_agg();
+    }
+    // the audit of the path board v (agent on the target: reached) of puzzle pr
+    __device__ uint32_t audit(const Params& p, const RulesTab& rt, const PuzzleRules<1>& pr, uint64_t v, bool reached,
+                              const uint8_t* simple) {
+        const uint32_t P = p.pitch;
+        const uint64_t cells = pr.pl[kB_CELLS].w[0];
+        const uint64_t a = (pr.pl[kB_LATTICE].w[0] & ~(pr.pl[kB_GAPS].w[0] | v)) | cells;
+        const uint64_t d = v ^ vis;
+        if (pr.q != q || (d & (d - 1ull)) != 0ull) {
+            rebuild(rt, pr, a, P);
+            q = pr.q;
+        } else if (d) {
+            const uint32_t pt = (uint32_t)__builtin_ctzll(d);
+            if (v & d) remove(rt, pr, a, pt, P, simple);
+            else add(rt, pr, a, pt, P);
+        }
+        vis = v;
+        BB<1> vb;
+        vb.w[0] = v;
+        uint32_t bits = audit_path<1>(P, pr, vb, reached) | ((agg & 3u) << 4) | (((agg >> 2) & 1u) << 7);
+        bits |= (uint32_t)((bits & 0xFFu) == 0xFFu) << 8;
+        bits |= ((agg >> 3) & 1u) << 9;
+        return bits;
+    }
+};
 
 // the audit with the agent at (x, y)
 template <int W, class Memo = NoMemo>

@@ -49,14 +49,11 @@ VARIANTS = {
                  "            if (false) {\n                if (pid != pr.q) pr = puzzle_rules<1>(p, rt, pid);")],
     # the W = 1 flood fill with the -y runs filled in one step too: the +y carry fill applied to the
     # bit-reversed board (v_bfrev_b32 per half), instead of one -y step per iteration
-    "downfill": [("sparc_rules.hpp", """                const uint64_t up = (((a + r) ^ a) & a) | r;
-                N.w[0] = up | (r >> 1) | (r << P) | (r >> P);""", """                const uint64_t up = (((a + r) ^ a) & a) | r;
-                auto rev64 = [](uint64_t x) {
-                    return ((uint64_t)__builtin_bitreverse32((uint32_t)x) << 32) | __builtin_bitreverse32((uint32_t)(x >> 32));
-                };
-                const uint64_t ra = rev64(a), rr = rev64(r);
-                const uint64_t dn = rev64((((ra + rr) ^ ra) & ra) | rr);
-                N.w[0] = up | dn | (r << P) | (r >> P);""")],
+    "downfill": [("sparc_rules.hpp", """    const uint64_t up = (((a + r) ^ a) & a) | r;
+    return (up | (r >> 1) | (r << P) | (r >> P)) & a;""", """    const uint64_t up = (((a + r) ^ a) & a) | r;
+    const uint64_t ra = __builtin_bitreverse64(a), ru = __builtin_bitreverse64(up);
+    const uint64_t run = __builtin_bitreverse64((((ra + ru) ^ ra) & ra) | ru);
+    return (run | (run << P) | (run >> P)) & a;""")],
     # the plane writer's piece loop unrolled twice (more stores in flight per wave)
     "obsun2": [("sparc_kernels.hip", """    const uint32_t dl = 256u / XY, dc = 256u - dl * XY;   // a 64-piece stride in envs / cells
     for (; f < total; f += 256u) {""", """    const uint32_t dl = 256u / XY, dc = 256u - dl * XY;   // a 64-piece stride in envs / cells
@@ -74,11 +71,11 @@ VARIANTS = {
     }""")],
     # k_rollout1s without the trie wave's priority (re-checked after IOR balanced the chains)
     # the look-ahead trie wave (step1la) on every LDS-table grid, not only on <= 64 workgroups
-    "la": [("sparc_kernels.hip", "if (lds_s && blocks <= 64) launch_s(k_rollout1s<TB, false, true, true, IOR>, d_act);",
+    "la": [("sparc_kernels.hip", "if (lds_s && blocks <= 64) launch_s1(k_rollout1s<TB, false, true, true, IOR, false, 1>, d_act);",
             "if (lds_s) launch_s(k_rollout1s<TB, false, true, true, IOR>, d_act);")],
     # "la" with the look-ahead gather issued by on-trie lanes only (off-trie lanes cannot take on
     # the next step): fewer L2 requests at 65,536 envs, one exec-masked branch per step
-    "lamask": [("sparc_kernels.hip", "if (lds_s && blocks <= 64) launch_s(k_rollout1s<TB, false, true, true, IOR>, d_act);",
+    "lamask": [("sparc_kernels.hip", "if (lds_s && blocks <= 64) launch_s1(k_rollout1s<TB, false, true, true, IOR, false, 1>, d_act);",
                 "if (lds_s) launch_s(k_rollout1s<TB, false, true, true, IOR>, d_act);"),
                ("sparc_trie.hpp", """        const uint2 rec = trieg[((base + (S & 0x7FFFu)) << 2) + __builtin_amdgcn_ubfe(an16, 4u, 2u)];
         nrx = rec.x;
@@ -113,8 +110,8 @@ VARIANTS = {
     "group16": [("sparc_kernels.hip", "constexpr int kGroup1s = 4;", "constexpr int kGroup1s = 16;")],
     "group8": [("sparc_kernels.hip", "constexpr int kGroup1s = 4;", "constexpr int kGroup1s = 8;")],
     # c2 (grids of at most 64 workgroups) on the plain trie wave instead of the look-ahead form
-    "nola": [("sparc_kernels.hip", "if (lds_s && blocks <= 64) launch_s(k_rollout1s<TB, false, true, true, IOR>, d_act);",
-              "if (lds_s && blocks <= 0) launch_s(k_rollout1s<TB, false, true, true, IOR>, d_act);")],
+    "nola": [("sparc_kernels.hip", "if (lds_s && blocks <= 64) launch_s1(k_rollout1s<TB, false, true, true, IOR, false, 1>, d_act);",
+              "if (lds_s && blocks <= 0) launch_s1(k_rollout1s<TB, false, true, true, IOR, false, 1>, d_act);")],
     "noprio": [("sparc_kernels.hip", """        __builtin_amdgcn_s_setprio(1);
         static_assert(!(C && LA),""", """        static_assert(!(C && LA),""")],
     # MoveLane1 (k_rollout1s move wave): the stack byte a pop needs (slot len-4) read one step
@@ -144,10 +141,6 @@ VARIANTS = {
         pending = pu != 0u;"""),
                  ("sparc_move1.hpp", "        return ((uint32_t)dl << 30) | ((at_tgt | rs) ? kHwTgt : 0u) | (pending ? kHwDone : 0u) | lw;",
                   "        return ((uint32_t)dl << 30) | ((at | rsu) << 24) | (pu << 25) | lw;")],
-    # k_rollout1s on grids of at most 64 256-env workgroups (c2): one wave pair + its I/O wave per
-    # 64-env workgroup (PR = 1), so the move, trie and I/O waves each get a SIMD of their own
-    "pr1": [("sparc_kernels.hip", "if (lds_s && blocks <= 64) launch_s(k_rollout1s<TB, false, true, true, IOR>, d_act);",
-             "if (lds_s && blocks <= 64) launch_s1(k_rollout1s<TB, false, true, true, IOR, false, 1>, d_act);")],
     # k_rollout1r with s_memtime stamps (timing only: the stats buffer receives, per wave, role |
     # total | barrier-wait | audit cycles at index N/2 + block * 16 + wave; tools/diag_r1r.py)
     "stamps": [

@@ -24,8 +24,9 @@ ap.add_argument("--time", action="store_true", help="print the mean launch time 
 ap.add_argument("--lib", default=None, help="path of a diagnostic build of libsparc_gym_amd.so")
 ap.add_argument("--rules", action="store_true", help="the rule audit after every step (rollout(rules=True))")
 ap.add_argument("--puzzles", type=int, default=1024, help="pool size (bench.make_pool: blocks of 1,024)")
-ap.add_argument("--variant", type=int, action="append", default=[],
-                help="sparc_set_variant(ctx, VARIANT, 1) before the launches (core.VARIANT_*; repeatable)")
+ap.add_argument("--variant", action="append", default=[],
+                help="sparc_set_variant(ctx, VARIANT, 1), or VARIANT:VALUE, before the launches "
+                     "(core.VARIANT_*; repeatable)")
 a = ap.parse_args()
 sizes, full, tb, obs = bench.CONFIGS[a.config]
 proc = bench.make_pool(a.puzzles, sizes, full)   # before torch / any GPU call (worker processes fork)
@@ -44,7 +45,8 @@ a.rules = a.rules or a.config in bench.RULE_CONFIGS
 table = pack_table(proc)
 vec = SPaRCVecEnv(a.envs, processed=proc, table=table, traceback=tb, observation="compact", rules=a.rules)
 for v in a.variant:
-    vec.core.set_variant(v, 1)
+    which, _, value = v.partition(":")
+    vec.core.set_variant(int(which), int(value or 1))
 gid = np.arange(a.envs, dtype=np.uint64)
 vec.reset(options={"puzzle_index": (gid * 2654435761 % len(proc)).astype(np.int64)})
 acts = torch.randint(0, 4, (a.launches + 1, a.chunk, a.envs), dtype=torch.uint8, device="cuda")
