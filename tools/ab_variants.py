@@ -141,6 +141,54 @@ VARIANTS = {
         pending = pu != 0u;"""),
                  ("sparc_move1.hpp", "        return ((uint32_t)dl << 30) | ((at_tgt | rs) ? kHwTgt : 0u) | (pending ? kHwDone : 0u) | lw;",
                   "        return ((uint32_t)dl << 30) | ((at | rsu) << 24) | (pu << 25) | lw;")],
+    # MoveLaneW (k_rolloutWs move wave) with the free board in 16 VGPRs instead of LDS (VERDICT
+    # r5 item 6): the window is a select of the dword pair around the agent, the toggle a
+    # select-and-xor; LDS keeps the board only across load / store
+    "regboard": [
+        ("sparc_movew.hpp", "    uint32_t* bd = nullptr;          // this lane's dword 0 (stride 64 dwords)",
+         """    uint32_t* bd = nullptr;          // this lane's dword 0 (stride 64 dwords)
+    uint32_t rb[16];
+    __device__ __forceinline__ uint32_t rget(uint32_t k) const {
+        uint32_t v = 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < 16u; ++j) v = k == j ? rb[j] : v;
+        return v;
+    }
+    __device__ __forceinline__ void rxor(uint32_t k, uint32_t m) {
+#pragma unroll
+        for (uint32_t j = 0; j < 16u; ++j) rb[j] ^= k == j ? m : 0u;
+    }"""),
+        ("sparc_movew.hpp", """        const uint32_t k = e >> 5;
+        const uint64_t pr = ((uint64_t)dw(k + 1u) << 32) | dw(k);
+        w = pr >> (e & 31u);""", """        const uint32_t k = e >> 5;
+        const uint64_t pr = ((uint64_t)rget(k + 1u) << 32) | rget(k);
+        w = pr >> (e & 31u);"""),
+        ("sparc_movew.hpp", "        __hip_atomic_fetch_xor(&dw(tog >> 5), moved << (tog & 31u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);",
+         "        rxor(tog >> 5, moved << (tog & 31u));"),
+        ("sparc_movew.hpp", """                if (4u * k < g.BS) {
+                    dw(4u * k) = nb[k].x;
+                    dw(4u * k + 1u) = nb[k].y;
+                    dw(4u * k + 2u) = nb[k].z;
+                    dw(4u * k + 3u) = nb[k].w;
+                }""", """                if (4u * k < g.BS) {
+                    rb[4u * k] = nb[k].x;
+                    rb[4u * k + 1u] = nb[k].y;
+                    rb[4u * k + 2u] = nb[k].z;
+                    rb[4u * k + 3u] = nb[k].w;
+                }"""),
+        ("sparc_movew.hpp", """        rs = 0;
+        read_window(g);
+    }""", """        rs = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 16u; ++j) rb[j] = j < g.BS ? dw(j) : 0u;
+        read_window(g);
+    }"""),
+        ("sparc_movew.hpp", """        const uint32_t sx = (inf.x >> 16) & 0xFFu, sy = inf.x >> 24;
+        uint64_t vis[W];""", """        const uint32_t sx = (inf.x >> 16) & 0xFFu, sy = inf.x >> 24;
+#pragma unroll
+        for (uint32_t j = 0; j < 16u; ++j)
+            if (j < g.BS) dw(j) = rb[j];
+        uint64_t vis[W];""")],
     # k_rollout1r with s_memtime stamps (timing only: the stats buffer receives, per wave, role |
     # total | barrier-wait | audit cycles at index N/2 + block * 16 + wave; tools/diag_r1r.py)
     "stamps": [
