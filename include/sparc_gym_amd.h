@@ -354,9 +354,12 @@ int sparc_set_rule_limits(void *ctx, uint32_t fit_cap_nodes, uint64_t table_entr
  *                                      the mixed trie tables (4-B records for tries of <= 127
  *                                      nodes) 0: when the 8-B records outgrow 4 MB (default),
  *                                      1: always, 2: never
+ *  SPARC_VARIANT_HOST_FITS             1: the answers of exact fits finished on the host are not
+ *                                      kept for later audits (every such search is queued again:
+ *                                      tests of the queue path); 0: default
  * SPARC_E_INVALID for another `which` or value. */
 enum { SPARC_VARIANT_IO_CODES_OFF = 1, SPARC_VARIANT_RULE_ROLLOUT_GENERIC = 2, SPARC_VARIANT_R1R_SHAPE = 3,
-       SPARC_VARIANT_OBS_INLINE = 4, SPARC_VARIANT_MIXED_TRIE = 5 };
+       SPARC_VARIANT_OBS_INLINE = 4, SPARC_VARIANT_MIXED_TRIE = 5, SPARC_VARIANT_HOST_FITS = 6 };
 int sparc_set_variant(void *ctx, int32_t which, int32_t value);
 
 /* ---- multi-GPU: the end-of-batch gather over RCCL (xGMI) -------------------------------------

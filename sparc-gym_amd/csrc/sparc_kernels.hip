@@ -1988,6 +1988,7 @@ struct Ctx {
     std::vector<uint4> h_hf;
     uint4* d_hf = nullptr;
     uint32_t hf_used = 0;
+    bool hostfits_off = false;    // SPARC_VARIANT_HOST_FITS = 1: answers not kept (tests: the queue path)
     // the one-env record of sparc_env_step / _reset / _read (pinned, written by the kernels)
     sparc_env_record* h_rec = nullptr;
     sparc_env_record* d_rec = nullptr;
@@ -2131,7 +2132,8 @@ RulesTab rules_tab(const Ctx* c, bool queue) {
     rt.reg_off = c->r_reg_off;
     rt.reg_tab = c->r_reg_tab;
     rt.fq = FitQueue{queue ? c->fq_count : nullptr, c->fq_items, c->fq_cap};
-    rt.hf = HostFits{c->d_hf, c->h_hf.empty() ? 0u : (uint32_t)c->h_hf.size() - 1u, c->d_hf ? c->hf_used : 0u};
+    rt.hf = c->hostfits_off ? HostFits{nullptr, 0u, 0u}
+                            : HostFits{c->d_hf, c->h_hf.empty() ? 0u : (uint32_t)c->h_hf.size() - 1u, c->d_hf ? c->hf_used : 0u};
     rt.rows = c->r_rows;
     return rt;
 }
@@ -3369,6 +3371,7 @@ bool hostfits_insert(std::vector<uint4>& t, uint32_t q, uint64_t rm, uint32_t fi
 // kept (audits then queue those searches again; the results are the same).
 constexpr size_t kHostFitsMin = (size_t)1 << 12, kHostFitsMax = (size_t)1 << 22;
 int hostfits_add(Ctx* c, const std::vector<std::pair<uint32_t, uint64_t>>& keys, const std::vector<int8_t>& res) {
+    if (c->hostfits_off) return SPARC_OK;
     const size_t need = (size_t)c->hf_used + keys.size();
     size_t cap = c->h_hf.size();
     if (2 * need > cap && cap < kHostFitsMax) {
@@ -3517,6 +3520,10 @@ int sparc_set_variant(void* ctx, int32_t which, int32_t value) {
         case SPARC_VARIANT_MIXED_TRIE:
             if (value < 0 || value > 2) break;
             c->mixed_trie = value;
+            return SPARC_OK;
+        case SPARC_VARIANT_HOST_FITS:
+            if (value != 0 && value != 1) break;
+            c->hostfits_off = value == 1;
             return SPARC_OK;
         default:
             return fail(c, SPARC_E_INVALID, "unknown variant");

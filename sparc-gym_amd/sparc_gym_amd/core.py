@@ -97,7 +97,7 @@ class SparcCore:
 
     # sparc_set_variant (include/sparc_gym_amd.h): kernel variants with identical results
     VARIANT_IO_CODES_OFF, VARIANT_RULE_ROLLOUT_GENERIC, VARIANT_R1R_SHAPE, VARIANT_OBS_INLINE = 1, 2, 3, 4
-    VARIANT_MIXED_TRIE = 5
+    VARIANT_MIXED_TRIE, VARIANT_HOST_FITS = 5, 6
 
     def set_variant(self, which, value):
         """Debug: select a kernel variant of identical results for this context (A/B, tests)."""

@@ -234,7 +234,9 @@ def test_exact_fit_queue_overflow_rerun(on_gpu, generic):
     (_two_walls: two searches per audit, none on the GPU; 15 x 15 lattices have no region-code
     table, so rule rollouts take the generic rule kernel) a rule rollout of 8,192 envs x 48 steps
     (393,216 audits) queues far more searches than the first queue holds, and so does one k_rules
-    audit of 65,536 envs.  Their outputs equal the default cap's (every search on the GPU)."""
+    audit of 65,536 envs.  Their outputs equal the default cap's (every search on the GPU).  The
+    host's answers are not kept here (SPARC_VARIANT_HOST_FITS = 1): kept, the reset's audit would
+    answer every later search of this pool (test_host_fit_answers_are_kept)."""
     from sparc_gym_amd import SPaRCVecEnv, synthetic
     from sparc_gym_amd.puzzles import process_puzzles
     recs = [r for r in map(_two_walls, synthetic.make_puzzles(200, seed=41, sizes=((7, 7),), full_properties=False,
@@ -250,6 +252,7 @@ def test_exact_fit_queue_overflow_rerun(on_gpu, generic):
         for cap in (1, None):
             v = SPaRCVecEnv(n, processed=proc, traceback=True, autoreset="next_step", observation="compact",
                             rules=True, max_steps=40, fit_cap=cap)
+            v.core.set_variant(v.core.VARIANT_HOST_FITS, 1)
             v.reset(options={"puzzle_index": pids})
             st = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
             r = v.rollout(T, acts, rules=True, stats=st)
@@ -273,6 +276,7 @@ def test_exact_fit_queue_overflow_rerun(on_gpu, generic):
         for cap in (1, None):
             v = SPaRCVecEnv(n, processed=proc, traceback=True, autoreset="next_step", observation="compact",
                             rules=True, max_steps=40, fit_cap=cap)
+            v.core.set_variant(v.core.VARIANT_HOST_FITS, 1)
             v.reset(options={"puzzle_index": pids})
             v.rollout(7, None, seed=3, record=False)
             o = v.rule_audit(region=True, fit=True)
