@@ -1358,12 +1358,15 @@ __global__ void __launch_bounds__(192 * PR) k_rollout1s(Params p, int32_t T, con
 // That audit — a flood fill per region and one table lookup per region (sparc_rules.hpp) — costs
 // about ten times the step and is one latency-bound dependency chain per lane, so it runs in
 // waves of its own: per 64 envs one STEP wave (Env<1>::advance: the step, the stats, the outputs)
-// and A AUDIT waves, audit wave q auditing the steps t with t % A == q.  Nothing is
-// computed twice and no audit wave carries step state.
+// and A AUDIT waves.  The audit waves take the workgroup's tile of env-steps in env-major order,
+// a wave's 64 lanes on consecutive steps of a few envs: their regions differ by a point or two,
+// so the lanes' flood fills run nearly in lock step (MI355X, c3r: 3.97 -> 2.97 ms per 2,000-step
+// launch against lanes on 64 envs at one step; profiles/r06/ab_c3r_em).  Nothing is computed
+// twice and no audit wave carries step state.
 //   The step wave hands every env-step over as one u64 and one u32 in LDS rings: the visited
 // board (the bits below kRingShift: every W = 1 pool with x_size * pitch <= 57) | the agent's bit
-// << 57, and the puzzle index after the step.  An audit wave reads only its own steps and keeps
-// the puzzle's rule row in registers while its env stays on a puzzle.  The step wave is
+// << 57, and the puzzle index after the step.  An audit lane keeps the rule row of its last
+// job's puzzle in registers (a job of another puzzle reloads it from the L2).  The step wave is
 // pipelined as k_rollout1's env waves (the trie phase of step t-1 next to the move phase of step
 // t), and keeps the reset board of its env's puzzle for the visited plane, so its tile of steps
 // stays shorter than the audit waves' (MI355X: with the fused step and the path rules moved onto
@@ -1374,7 +1377,7 @@ __global__ void __launch_bounds__(192 * PR) k_rollout1s(Params p, int32_t T, con
 // three reward / flag buffers, as tile k-1's last reward code is written in interval k), the
 // audit waves audit tile k-1.  Only the step waves read and write the env state.
 // Shape <G, A, RT>: G 64-env groups per workgroup, A audit waves per group (so G * (1 + A) waves
-// <= 16), RT steps per tile (a multiple of A).
+// <= 16), RT steps per tile (a multiple of A: RT / A audits per audit lane and tile).
 template <int G, int A, int RT>
 struct R1Geom {
     static_assert(G * (1 + A) <= 16 && RT % A == 0, "k_rollout1r shape");
@@ -1612,22 +1615,33 @@ __global__ void __launch_bounds__(64 * G * (1 + A)) __attribute__((amdgpu_waves_
         }
         return;
     }
+    // The tile's RT * E audits in env-major order (job J: env column J / RT, step J % RT), the 64
+    // lanes of a wave on 64 consecutive jobs: the consecutive steps of a few envs, whose regions
+    // differ by a point or two, so the lanes' flood fills and region counts run nearly in lock
+    // step (tools/audit_lockstep_sim.py, random walks on 7 x 7 lattices: 15.7 lock-step flood
+    // iterations per wave-audit against 22.8 with a wave's lanes on 64 envs at one step)
+    constexpr uint32_t kSlots = (uint32_t)(A * G) * 64u;         // audit lanes per workgroup
+    const uint32_t s0 = (wv - (uint32_t)G) * 64u + lane;         // this lane's first job
+    (void)q;
     for (int32_t k = 1; k <= K; ++k) {
         const int32_t kt = k - 1, cnt = tile_cnt(kt);
         const uint32_t b = (uint32_t)kt & 1u;
 #pragma unroll 1
-        for (int32_t j = (int32_t)q; j < cnt; j += A) {          // this wave's steps of the tile
-            const uint64_t w = ring[at(b, j, col)];
-            const uint32_t pid = rpid[at(b, j, col)];
+        for (uint32_t J = s0; J < (uint32_t)RT * E; J += kSlots) {   // RT / A jobs per lane
+            const uint32_t ec = J / (uint32_t)RT, jj = J - ec * (uint32_t)RT;
+            const int32_t j = (int32_t)jj;
+            if (j >= cnt) continue;                               // a partial last tile
+            const uint64_t w = ring[at(b, j, ec)];
+            const uint32_t pid = rpid[at(b, j, ec)];
             uint32_t out = 0;
-            if (active) {
+            if (wg_base + ec < n) {
                 if (pid != pr.q) pr = puzzle_rules<1>(p, rt, pid);
                 BB<1> vb;
                 vb.w[0] = w & ((1ull << kRingShift) - 1ull);
                 const uint32_t ab = (uint32_t)(w >> kRingShift) & 63u;
                 out = audit_r<1, NoMemo, true>(p, rt, pr, vb, ab == pr.tbit, nullptr, nullptr).bits;
             }
-            tbt[at(b, j, col)] = (uint16_t)out;
+            tbt[at(b, j, ec)] = (uint16_t)out;
         }
         __syncthreads();                                         // B_{k+1}
     }

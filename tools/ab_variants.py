@@ -45,7 +45,7 @@ VARIANTS = {
     # the audit's flood fill cut to one dilation per region
     "noflood": [("sparc_rules.hpp", "            if (N == R) break;\n            R = N;", "            R = N;\n            break;")],
     # k_rollout1r audit waves do no audit at all (the step wave, rings and barriers only)
-    "noaudit": [("sparc_kernels.hip", "            if (active) {\n                if (pid != pr.q) pr = puzzle_rules<1>(p, rt, pid);",
+    "noaudit": [("sparc_kernels.hip", "            if (wg_base + ec < n) {\n                if (pid != pr.q) pr = puzzle_rules<1>(p, rt, pid);",
                  "            if (false) {\n                if (pid != pr.q) pr = puzzle_rules<1>(p, rt, pid);")],
     # the W = 1 flood fill with the -y runs filled in one step too: the +y carry fill applied to the
     # bit-reversed board (v_bfrev_b32 per half), instead of one -y step per iteration
@@ -226,16 +226,16 @@ VARIANTS = {
     __syncthreads();                                             // B_0
     { const uint64_t s0_ = __builtin_amdgcn_s_memtime(); __syncthreads(); dg_bar += __builtin_amdgcn_s_memtime() - s0_; }"""),
         ("sparc_kernels.hip", """            uint32_t out = 0;
-            if (active) {
+            if (wg_base + ec < n) {
                 if (pid != pr.q) pr = puzzle_rules<1>(p, rt, pid);""", """            uint32_t out = 0;
             const uint64_t sa_ = __builtin_amdgcn_s_memtime();
-            if (active) {
+            if (wg_base + ec < n) {
                 if (pid != pr.q) pr = puzzle_rules<1>(p, rt, pid);"""),
-        ("sparc_kernels.hip", """            tbt[at(b, j, col)] = (uint16_t)out;
+        ("sparc_kernels.hip", """            tbt[at(b, j, ec)] = (uint16_t)out;
         }
         __syncthreads();                                         // B_{k+1}
     }
-}""", """            tbt[at(b, j, col)] = (uint16_t)out;
+}""", """            tbt[at(b, j, ec)] = (uint16_t)out;
             dg_aud += __builtin_amdgcn_s_memtime() - sa_;
         }
         { const uint64_t s0_ = __builtin_amdgcn_s_memtime(); __syncthreads(); dg_bar += __builtin_amdgcn_s_memtime() - s0_; }
