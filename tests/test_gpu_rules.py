@@ -172,9 +172,10 @@ def test_rollout_rule_bits_every_step(on_gpu, sizes, max_shaped):
 
 @pytest.mark.parametrize("n", [200, 1000, 1040])
 def test_rollout_rule_bits_ragged_batches(on_gpu, n):
-    """Rule rollouts over batches that are not whole workgroups (two audit waves per 64 envs, each
-    auditing every other step): 200 and 1000 envs (not multiples of 16: every step goes through the
-    per-step path), 1040 (tiled, with a last wave pair of 16 envs), an odd T split over two
+    """Rule rollouts over batches that are not whole workgroups (k_rollout1r: the audit waves take
+    a tile's env-steps in env-major order, so the jobs of missing envs and of a partial last tile
+    are skipped inside a wave): 200 and 1000 envs (not multiples of 16: every step goes through the
+    per-step path), 1040 (tiled, with a last group of 16 envs), an odd T split over two
     launches; the bits after every step equal step()-by-step() audits and the reward codes /
     flags / stats equal a plain rollout's."""
     from sparc_gym_amd import SPaRCVecEnv, synthetic
