@@ -7,14 +7,12 @@ For the 7 x 7 (c3 pool) and 15 x 15 (c3g7 pool) puzzles, observation 'new' and '
 rule_status True / False, it runs random-action episodes (reset on done) and reports the mean
 wall time of step() and of reset().  Beside it: the bare C calls of one step (sparc_env_step with
 and without the audit, one stream synchronisation each) against the previous composition
-(sparc_step_host + sparc_read_state + sparc_rules_host: four or more synchronisations), and, on
-the same host, the reference-speed pure-Python restatement of step() (oracle/cpu_ref.py, one
-core) without and with the rule audit twice per step as the reference runs it.  One JSON line
-per measurement."""
+(sparc_step_host + sparc_read_state + sparc_rules_host: four or more synchronisations).  One JSON
+line per measurement.  (The CPU side of the comparison is bench.py's cpu_baseline leg: the c3r
+line times the reference-speed restatement of step() with its two audits per step.)"""
 import argparse
 import json
 import os
-import subprocess
 import sys
 import time
 
@@ -31,7 +29,6 @@ POOLS = {"7x7": ((3, 3),), "15x15": ((7, 7),)}
 ap = argparse.ArgumentParser()
 ap.add_argument("--steps", type=int, default=2000)
 ap.add_argument("--puzzles", type=int, default=256)
-ap.add_argument("--cpu-seconds", type=float, default=5.0)
 a = ap.parse_args()
 
 
@@ -92,13 +89,3 @@ for pool, sizes in POOLS.items():
             emit(kind="c_abi", pool=pool, audit=audit,
                  calls="step_host+read_state" + ("+rules_host" if audit else "") if legacy else "env_step",
                  us=round(t / a.steps * 1e6, 1))
-
-# the reference-speed CPU restatement of step() on one core of this host (oracle/cpu_ref.py; the
-# test / benchmark oracle, run as a child process: nothing of it is loaded here)
-for impl in ("py", "py_rules"):
-    out = subprocess.run([sys.executable, "-m", "oracle.cpu_bench", "--config", "c3", "--procs", "1",
-                          "--seconds", str(a.cpu_seconds), "--impl", impl, "--puzzles", str(a.puzzles)],
-                         cwd=REPO, capture_output=True, text=True, check=True)
-    r = json.loads(out.stdout.strip().splitlines()[-1])
-    emit(kind="cpu_restatement", impl=impl, pool="7x7", steps_per_s=r["value"],
-         us=round(1e6 / r["value"], 1), cores=1)
