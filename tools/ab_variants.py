@@ -189,13 +189,6 @@ VARIANTS = {
         for (uint32_t j = 0; j < 16u; ++j)
             if (j < g.BS) dw(j) = rb[j];
         uint64_t vis[W];""")],
-    # k_rollout1r audit lanes on one env each (env s / A, steps s % A + m * A: a wave-iteration on
-    # A consecutive steps of 64 / A envs), so a lane's rule row is reloaded only when its env
-    # changes puzzle, against the product's 64 consecutive env-major jobs (a new env per job)
-    "strided": [("sparc_kernels.hip", """        for (uint32_t J = s0; J < (uint32_t)RT * E; J += kSlots) {   // RT / A jobs per lane
-            const uint32_t ec = J / (uint32_t)RT, jj = J - ec * (uint32_t)RT;""",
-                 """        for (uint32_t jj = s0 % (uint32_t)A; jj < (uint32_t)RT; jj += (uint32_t)A) {
-            const uint32_t ec = s0 / (uint32_t)A;""")],
     # k_rollout1r with s_memtime stamps (timing only: the stats buffer receives, per wave, role |
     # total | barrier-wait | audit cycles at index N/2 + block * 16 + wave; tools/diag_r1r.py)
     "stamps": [
