@@ -88,6 +88,8 @@ def parse():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--mode", default="rollout", choices=["rollout", "step"])
     ap.add_argument("--puzzles", type=int, default=1024)
+    ap.add_argument("--placement", default="auto", choices=["auto", "hash", "xcd"],
+                    help="first puzzle of each env (initial_puzzles): auto = xcd past 1,024 puzzles")
     ap.add_argument("--max-steps", type=int, default=2000)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -97,6 +99,26 @@ def parse():
     if a.mode == "step" and a.config in RULE_CONFIGS:
         ap.error(f"--mode step runs no rule audit: {a.config} needs --mode rollout")
     return a
+
+
+def initial_puzzles(gid, P, placement):
+    """Each env's first puzzle (the rest follow by next-step autoreset, pid + 1 mod P).
+    'hash': env g -> (g * 2654435761) mod P.  'xcd': the same hash within one eighth of the pool
+    per XCD: the split kernel runs 256 envs per workgroup and workgroups b, b + 8, ... share an XCD
+    (round-robin dispatch, MI355X_MICROARCH.md), so local env slot s starts on a puzzle of block
+    ((s // 256) % 8) of the pool and an XCD's L2 holds the records of about P / 8 puzzles instead of
+    all P.  Every puzzle still starts 65,536 / P envs; only which env slot plays it changes.
+    'auto': 'xcd' for pools past the 1,024 LDS-staged rows (P % 8 == 0), else 'hash'."""
+    gid = np.asarray(gid, dtype=np.uint64)
+    if placement == "auto":
+        placement = "xcd" if P > 1024 and P % 8 == 0 else "hash"
+    if placement == "hash" or P < 8:
+        return (gid * np.uint64(2654435761) % np.uint64(P)).astype(np.int64), "hash"
+    span = P // 8
+    slot = gid - gid[0] if len(gid) else gid
+    grp = (slot // np.uint64(256)) % np.uint64(8)
+    k = (slot // np.uint64(2048)) * np.uint64(256) + slot % np.uint64(256)   # the env's index in its XCD group
+    return (grp * np.uint64(span) + k * np.uint64(2654435761) % np.uint64(span)).astype(np.int64), "xcd"
 
 
 def rule_rollout_kernel(proc, table):
@@ -473,7 +495,8 @@ def main():
     vec = SPaRCVecEnv(n, processed=proc, table=table, traceback=tb, max_steps=args.max_steps,
                       autoreset="next_step", device=local, env_offset=offset, observation="compact")
     gid = np.arange(offset, offset + n, dtype=np.uint64)
-    vec.reset(options={"puzzle_index": (gid * 2654435761 % len(proc)).astype(np.int64)})
+    pidx, placement = initial_puzzles(gid, len(proc), args.placement)
+    vec.reset(options={"puzzle_index": pidx})
 
     K, W = max(1, args.steps), max(0, args.warmup)
     # env-steps per env in one bench step (one launch)
@@ -588,6 +611,8 @@ def main():
     workload = f"{args.config}_{args.mode}_n{n}_chunk{chunk if args.mode == 'rollout' else 1}"
     if args.puzzles != 1024:   # the counters of another pool size are recorded under their own key
         workload += f"_p{args.puzzles}"
+    if placement == "xcd":
+        workload += "_xcd"
     pmc = load_traffic(workload, kernel)
     traffic = pmc["bytes"] if pmc else None
     issue = None
@@ -633,6 +658,7 @@ def main():
         "config": {"workload": f"{args.config}: {n} envs/GPU, lattices {['%dx%d' % (2*w+1, 2*h+1) for w, h in sizes]}, "
                                f"{'full property set' if full else 'base planes'}, traceback={tb}, "
                                f"max_steps={args.max_steps}, next-step autoreset, {args.puzzles} puzzles"
+                               + (", XCD-local first puzzles (bench.initial_puzzles)" if placement == "xcd" else "")
                                + (f", observation='new': visited + agent_location int32 planes "
                                   f"[N, {X}, {Y}] written every step" if obs else "")
                                + (", rule audit (info['rule_status'] bits, SPaRC_Gym.py:941-950) after "

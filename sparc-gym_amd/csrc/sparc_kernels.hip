@@ -1585,6 +1585,10 @@ __global__ void __launch_bounds__(64 * G * (1 + A)) __attribute__((amdgpu_waves_
     }
 
     // ---- audit waves
+    // the audit waves set the pace (the step waves alone: 1.30 ms per 2,000-step launch), so they
+    // win VALU arbitration against their step wave (MI355X, c3r: 2.72 -> 2.58 ms per launch,
+    // profiles/r06/ab_c3r_flood)
+    __builtin_amdgcn_s_setprio(1);
     const uint32_t q = wv / (uint32_t)G - 1u;                    // audits the steps t % A == q (INC: block q)
     PuzzleRules<1> pr;
     pr.q = 0xFFFFFFFFu;
@@ -1952,7 +1956,8 @@ struct Ctx {
     // pools past the LDS row budget
     uint8_t* t_trie4 = nullptr;
     uint4* t_trow4 = nullptr;
-    bool mixed_pays = false;   // the 8-B records outgrow an XCD's L2 (sparc_load_puzzles)
+    bool mixed_pays = false;   // the 8-B records outgrow an XCD's L2 (sparc_load_puzzles, sparc_reset_host)
+    std::vector<uint32_t> nodes8;   // W = 1: trie nodes (8-B records) per puzzle, for the XCD hot set
     int mixed_trie = 0;        // SPARC_VARIANT_MIXED_TRIE: 0 when it pays, 1 always, 2 never
     uint4 *t_trow = nullptr, *t_mrow = nullptr;
     // multi-word split kernel (k_rolloutWs): move rows and reset boards; split_w false when the
@@ -2128,6 +2133,9 @@ struct R1Shape {
 
 constexpr uint64_t kFitQueueCap = 1u << 16;   // exact fits past the node cap per audit call (grown)
 constexpr size_t kMixedTrieBytes = (size_t)4 << 20;   // an XCD's L2: past it the mixed trie tables pay
+// puzzles an env plays per 2,000-step launch under random actions (episodes of ~300 steps, next
+// puzzle on each autoreset): the window of its start puzzle that xcd_hot_bytes counts
+constexpr uint32_t kHotWalk = 8;
 constexpr uint64_t kFitQueueMax = (uint64_t)1 << 28;   // 6 GB of FitTodo
 
 // the loaded rule table as the kernels take it; queue: push searches past the node cap to the
@@ -2357,6 +2365,7 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
     c->t_trie4 = nullptr;
     c->t_trow4 = nullptr;
     c->mixed_pays = false;
+    c->nodes8.clear();
     if (c->t_trow) HIPCHK(c, hipFree(c->t_trow));
     if (c->t_mrow) HIPCHK(c, hipFree(c->t_mrow));
     if (c->t_mroww) HIPCHK(c, hipFree(c->t_mroww));
@@ -2528,6 +2537,10 @@ int sparc_load_puzzles(void* ctx, const sparc_puzzle_table* t) {
         // more than the misses it saves (MI355X, c3: 4,096 puzzles, 2 MB of records, +5 %; 16,384
         // puzzles, 8.4 MB, -7.4 %; profiles/r06/ab_bigpool); SPARC_VARIANT_MIXED_TRIE overrides
         c->mixed_pays = nn8 * sizeof(uint2) > kMixedTrieBytes;
+        if (W == 1 && c->mixed_pays) {   // sparc_reset_host refines the choice per XCD (xcd_hot_bytes)
+            c->nodes8.resize(P);
+            for (size_t q = 0; q < P; ++q) c->nodes8[q] = t->info[4 * q + 3] & 0xFFFFu;
+        }
         if (W == 1) {
             std::vector<size_t> bo(P, 0);
             size_t nb = 0;
@@ -2650,6 +2663,29 @@ int sparc_reset_device(void* ctx, const uint32_t* d_q, const uint8_t* d_mask, ui
     return SPARC_OK;
 }
 
+// The 8-B trie records one XCD's L2 must hold for the envs of a full reset: k_rollout1s runs 256
+// envs per workgroup and workgroups b, b + 8, ... share an XCD (round-robin dispatch,
+// MI355X_MICROARCH.md), so XCD group g holds envs i with (i / 256) % 8 == g, and each env plays
+// its start puzzle and the next kHotWalk - 1.  Returns the largest group's bytes.  A pool whose
+// envs are placed XCD-locally (bench.initial_puzzles 'xcd') keeps the 8-B records past 4 MB of
+// them (MI355X, c3 at 16,384 puzzles: 0.362 ms with 8-B records against 0.379 ms mixed; the
+// hash placement 0.405 ms, mixed 0.394; profiles/r06/ab_xcd_place).
+static size_t xcd_hot_bytes(const Ctx* c, const uint32_t* q) {
+    const uint32_t P = c->num_puzzles;
+    std::vector<uint8_t> seen(P, 0);   // bit g: counted for group g
+    size_t bytes[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint32_t i = 0; i < c->n; ++i) {
+        const uint32_t g = (i / 256u) & 7u;
+        uint32_t u = q[i];
+        for (uint32_t k = 0; k < kHotWalk; ++k, u = u + 1 == P ? 0u : u + 1) {
+            if (seen[u] & (1u << g)) continue;
+            seen[u] |= (uint8_t)(1u << g);
+            bytes[g] += (size_t)c->nodes8[u] * sizeof(uint2);
+        }
+    }
+    return *std::max_element(bytes, bytes + 8);
+}
+
 int sparc_reset_host(void* ctx, const uint32_t* q, const uint8_t* mask, uint8_t* flags) {
     DevGuard dg;
     Ctx* c = static_cast<Ctx*>(ctx);
@@ -2658,6 +2694,7 @@ int sparc_reset_host(void* ctx, const uint32_t* q, const uint8_t* mask, uint8_t*
     if (!q) return fail(c, SPARC_E_INVALID, "null puzzle_index");
     for (uint32_t i = 0; i < c->n; ++i)
         if ((!mask || mask[i]) && q[i] >= c->num_puzzles) return fail(c, SPARC_E_INVALID, "puzzle index out of range");
+    if (!mask && c->nodes8.size() == c->num_puzzles) c->mixed_pays = xcd_hot_bytes(c, q) > kMixedTrieBytes;
     HIPCHK(c, hipMemcpyAsync(c->s_pidx, q, sizeof(uint32_t) * c->n, hipMemcpyHostToDevice, c->stream));
     if (mask) HIPCHK(c, hipMemcpyAsync(c->s_mask, mask, c->n, hipMemcpyHostToDevice, c->stream));
     rc = sparc_reset_device(c, c->s_pidx, mask ? c->s_mask : nullptr, flags ? c->s_flags : nullptr);

@@ -583,9 +583,16 @@ __device__ __forceinline__ uint32_t audit_path(uint32_t P, const PuzzleRules<W>&
 // each way 39.9, +y runs 34.4.  The -y runs by the same add on the bit-reversed board (two more
 // 64-bit adds and four bit reversals per iteration) cost more than the iterations they save:
 // MI355X, c3r 2,000-step launches 3.956 -> 4.11-4.14 ms (profiles/r06/ab_c3r_inc).
+// (a & ~(a + r)) | r | (x & a) = (a & ~((a + r) & ~x)) | r (r lies in a): one v_bitop3 per half,
+// 6 logic VALU against the compiler's 8 (two v_not, four v_or3, two v_and); with the flood loop
+// two dilations per trip (audit_r) c3r 2.97 -> 2.72 ms per 2,000-step launch (bitop3 alone 2.88,
+// the loop alone 2.93; profiles/r06/ab_c3r_flood)
 __device__ __forceinline__ uint64_t dilate_w1(uint64_t r, uint64_t a, uint32_t P) {
-    const uint64_t up = (((a + r) ^ a) & a) | r;
-    return (up | (r >> 1) | (r << P) | (r >> P)) & a;
+    const uint64_t s = a + r, x = (r >> 1) | (r << P) | (r >> P);
+    uint32_t lo, hi;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xb0" : "=v"(lo) : "v"((uint32_t)a), "v"((uint32_t)s), "v"((uint32_t)x));
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xb0" : "=v"(hi) : "v"((uint32_t)(a >> 32)), "v"((uint32_t)(s >> 32)), "v"((uint32_t)(x >> 32)));
+    return ((((uint64_t)hi) << 32) | lo) | r;
 }
 
 // vis: path points; reached: the agent is on the target (_rule_reached_target 487-495); pr: the
@@ -633,7 +640,18 @@ __device__ RuleOut<W> audit_r(const Params& p, const RulesTab& rt, const PuzzleR
     while (remaining.any()) {
         BB<W> R = BB<W>::zero();
         R.set(remaining.lowest());
-        while (true) {                                           // flood fill (BFS 431-452)
+        if constexpr (W == 1) {   // two dilations per trip: no register copy of R per iteration
+            // (four per trip measured slower: 2.77 against 2.72 ms, profiles/r06/ab_c3r_flood)
+            uint64_t r0 = R.w[0];
+            const uint64_t aw = allowed.w[0];
+            while (true) {
+                const uint64_t r1 = dilate_w1(r0, aw, P);
+                if (r1 == r0) break;
+                r0 = dilate_w1(r1, aw, P);
+                if (r0 == r1) break;
+            }
+            R.w[0] = r0;
+        } else while (true) {                                    // flood fill (BFS 431-452)
             BB<W> N;
             if constexpr (W == 1)
                 N.w[0] = dilate_w1(R.w[0], allowed.w[0], P);   // whole +y runs per iteration

@@ -67,12 +67,14 @@ def _sharded_oracle(proc, pids, acts_list, tb, ms, shards=16):
     return outs, np.concatenate(stats), {k: np.concatenate([s[k] for s in states]) for k in states[0]}
 
 
-@pytest.mark.parametrize("P", [4096, 16384])
-def test_c3_full_size_big_puzzle_pool_vs_oracle(on_gpu, P):
+@pytest.mark.parametrize("P,placement", [(4096, "hash"), (16384, "hash"), (16384, "xcd")])
+def test_c3_full_size_big_puzzle_pool_vs_oracle(on_gpu, P, placement):
     """c3 (65,536 envs, 7x7 full property set, traceback, max_steps 2,000, next-step autoreset)
     on a 4,096- and a 16,384-puzzle pool (bench.make_pool: the bench's 1,024-puzzle pool and more
     blocks; 16,384 is the pool of the bench line whose trie records outgrow an XCD's L2), env i ->
-    puzzle i * 2654435761 mod P, actions drawn as the bench's, two back-to-back 2,000-step
+    puzzle i * 2654435761 mod P ('hash': the mixed 4-/8-B trie records) or the bench's XCD-local
+    first puzzles ('xcd', bench.initial_puzzles: one eighth of the pool per XCD, so the reset keeps
+    the 8-B records, xcd_hot_bytes), actions drawn as the bench's, two back-to-back 2,000-step
     launches through the bench's C-ABI call: every env bit-exact against the C oracle
     (SPaRC_Gym.py:1111-1238, reset 1087)."""
     import bench
@@ -82,7 +84,8 @@ def test_c3_full_size_big_puzzle_pool_vs_oracle(on_gpu, P):
     table = pack_table(proc)
     assert len(proc) == P > LDS_ROW_LIMIT and table.words == 1
     n, T, L = 65536, 2000, 2
-    pids = (np.arange(n, dtype=np.uint64) * 2654435761 % len(proc)).astype(np.int64)
+    pids, used = bench.initial_puzzles(np.arange(n, dtype=np.uint64), len(proc), placement)
+    assert used == placement
     v = SPaRCVecEnv(n, processed=proc, table=table, traceback=True, max_steps=2000, autoreset="next_step",
                     observation="compact")
     v.reset(options={"puzzle_index": pids})

@@ -43,17 +43,15 @@ VARIANTS = {
     "noreload": [("sparc_kernels.hip", "                if (pid != pr.q) pr = puzzle_rules<1>(p, rt, pid);",
                   "                if (pr.q == 0xFFFFFFFFu) pr = puzzle_rules<1>(p, rt, pid);")],
     # the audit's flood fill cut to one dilation per region
-    "noflood": [("sparc_rules.hpp", "            if (N == R) break;\n            R = N;", "            R = N;\n            break;")],
+    "noflood": [("sparc_rules.hpp", """            while (true) {
+                const uint64_t r1 = dilate_w1(r0, aw, P);
+                if (r1 == r0) break;
+                r0 = dilate_w1(r1, aw, P);
+                if (r0 == r1) break;
+            }""", "            r0 = dilate_w1(r0, aw, P);")],
     # k_rollout1r audit waves do no audit at all (the step wave, rings and barriers only)
     "noaudit": [("sparc_kernels.hip", "            if (wg_base + ec < n) {\n                if (pid != pr.q) pr = puzzle_rules<1>(p, rt, pid);",
                  "            if (false) {\n                if (pid != pr.q) pr = puzzle_rules<1>(p, rt, pid);")],
-    # the W = 1 flood fill with the -y runs filled in one step too: the +y carry fill applied to the
-    # bit-reversed board (v_bfrev_b32 per half), instead of one -y step per iteration
-    "downfill": [("sparc_rules.hpp", """    const uint64_t up = (((a + r) ^ a) & a) | r;
-    return (up | (r >> 1) | (r << P) | (r >> P)) & a;""", """    const uint64_t up = (((a + r) ^ a) & a) | r;
-    const uint64_t ra = __builtin_bitreverse64(a), ru = __builtin_bitreverse64(up);
-    const uint64_t run = __builtin_bitreverse64((((ra + ru) ^ ra) & ra) | ru);
-    return (run | (run << P) | (run >> P)) & a;""")],
     # the plane writer's piece loop unrolled twice (more stores in flight per wave)
     "obsun2": [("sparc_kernels.hip", """    const uint32_t dl = 256u / XY, dc = 256u - dl * XY;   // a 64-piece stride in envs / cells
     for (; f < total; f += 256u) {""", """    const uint32_t dl = 256u / XY, dc = 256u - dl * XY;   // a 64-piece stride in envs / cells

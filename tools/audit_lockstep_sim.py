@@ -62,6 +62,16 @@ class Env:
         for (x,y) in s.path: v|=1<<(x*P+y)
         a=(lattice&~(s.g|v))|cells
         return regions(cells,a,P)
+def flat(jobs):
+    # one loop over dilations: a lane that converges finishes its region and seeds the next in the
+    # same iteration; cost = the longest lane's total, and the finish block runs in every
+    # iteration where some lane ends a region
+    ends=set()
+    for j in jobs:
+        t=0
+        for it in j:
+            t+=it; ends.add(t)
+    return max(sum(j) for j in jobs), len(ends)
 def lockstep(jobs):
     # jobs: list of region-iteration lists; cost = sum over k of max iters, + per-region overhead
     K=max(len(j) for j in jobs)
@@ -226,6 +236,7 @@ def pool_mode(envs=1280, tiles=20, RT=10, A=5, seed=3):
             e.step()
     fixed = consec = 0
     useful = 0
+    fl_it = fl_fin = ns_reg = 0
     for t in range(tiles):
         costs = [[None] * envs for _ in range(RT)]
         for j in range(RT):
@@ -237,10 +248,18 @@ def pool_mode(envs=1280, tiles=20, RT=10, A=5, seed=3):
             for g in range(envs // 64):
                 fixed += lockstep(costs[j][g * 64:(g + 1) * 64])[0]
         for w0 in range(0, envs * RT, 64):      # env-major: 64 consecutive (env, step) jobs
-            consec += lockstep([costs[J % RT][J // RT] for J in range(w0, w0 + 64)])[0]
+            jobs = [costs[J % RT][J // RT] for J in range(w0, w0 + 64)]
+            it, K = lockstep(jobs)
+            consec += it
+            ns_reg += K
+            a, b = flat(jobs)
+            fl_it += a
+            fl_fin += b
     nj = tiles * RT * envs / 64
     print("c3r pool: useful iters per lane-audit %.2f; lock-step per wave-audit: lanes on 64 envs at one "
           "step %.2f, env-major %.2f" % (useful / (tiles * RT * envs), fixed / nj, consec / nj))
+    print("env-major nested: %.2f iterations + %.2f region finishes per wave-audit; flattened: %.2f "
+          "iterations, %.2f of them with a region finish" % (consec / nj, ns_reg / nj, fl_it / nj, fl_fin / nj))
 
 
 if __name__ == "__main__":

@@ -24,6 +24,7 @@ ap.add_argument("--time", action="store_true", help="print the mean launch time 
 ap.add_argument("--lib", default=None, help="path of a diagnostic build of libsparc_gym_amd.so")
 ap.add_argument("--rules", action="store_true", help="the rule audit after every step (rollout(rules=True))")
 ap.add_argument("--puzzles", type=int, default=1024, help="pool size (bench.make_pool: blocks of 1,024)")
+ap.add_argument("--placement", default="auto", choices=["auto", "hash", "xcd"], help="bench.initial_puzzles")
 ap.add_argument("--variant", action="append", default=[],
                 help="sparc_set_variant(ctx, VARIANT, 1), or VARIANT:VALUE, before the launches "
                      "(core.VARIANT_*; repeatable)")
@@ -48,7 +49,7 @@ for v in a.variant:
     which, _, value = v.partition(":")
     vec.core.set_variant(int(which), int(value or 1))
 gid = np.arange(a.envs, dtype=np.uint64)
-vec.reset(options={"puzzle_index": (gid * 2654435761 % len(proc)).astype(np.int64)})
+vec.reset(options={"puzzle_index": bench.initial_puzzles(gid, len(proc), a.placement)[0]})
 acts = torch.randint(0, 4, (a.launches + 1, a.chunk, a.envs), dtype=torch.uint8, device="cuda")
 rew = torch.empty((a.chunk, a.envs), dtype=torch.int8, device="cuda")
 flg = torch.empty((a.chunk, a.envs), dtype=torch.uint8, device="cuda")
