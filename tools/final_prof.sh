@@ -16,6 +16,8 @@ for spec in ${PROF_SPECS:-"c3:65536:2000:k_rollout1s" "c2:4096:2000:k_rollout1s"
   key=${cfg}_rollout_n${envs}_chunk${chunk}
   name=$cfg
   if [ "$pz" != 1024 ]; then key=${key}_p$pz; name=${cfg}_p$pz; fi
+  # pools past 1,024 puzzles run the XCD-local first puzzles (bench.initial_puzzles, auto), as bench.py keys them
+  if [ "$pz" -gt 1024 ] && [ $((pz % 8)) = 0 ]; then key=${key}_xcd; fi
   PUZZLES=$pz step prof_$name 420 bash tools/collect_profiles.sh gpurun_out/prof_$name $cfg $envs $chunk 5
   d=gpurun_out/prof_$name
   step fold_$name 60 python tools/pmc_traffic.py $key $kern $d/pmc_fetch.csv $d/pmc_write.csv $d/pmc_rdreq.csv $d/pmc_sq1.csv $d/pmc_sq2.csv
