@@ -102,23 +102,20 @@ def parse():
 
 
 def initial_puzzles(gid, P, placement):
-    """Each env's first puzzle (the rest follow by next-step autoreset, pid + 1 mod P).
-    'hash': env g -> (g * 2654435761) mod P.  'xcd': the same hash within one eighth of the pool
-    per XCD: the split kernel runs 256 envs per workgroup and workgroups b, b + 8, ... share an XCD
-    (round-robin dispatch, MI355X_MICROARCH.md), so local env slot s starts on a puzzle of block
-    ((s // 256) % 8) of the pool and an XCD's L2 holds the records of about P / 8 puzzles instead of
-    all P.  Every puzzle still starts 65,536 / P envs; only which env slot plays it changes.
-    'auto': 'xcd' for pools past the 1,024 LDS-staged rows (P % 8 == 0), else 'hash'."""
+    """Each env's first puzzle (the rest follow by next-step autoreset, pid + 1 mod P); gid: this
+    rank's global env ids.  'hash': env g -> (g * 2654435761) mod P.  'xcd':
+    sparc_gym_amd.vec_env.xcd_local_puzzle_index, the same hash within one eighth of the pool per
+    XCD group of workgroups, so an XCD's L2 holds the records of about P / 8 puzzles; every puzzle
+    still starts 65,536 / P envs, only the env slot that plays it changes.  'auto': 'xcd' for
+    pools past the 1,024 LDS-staged rows (P % 8 == 0), else 'hash'."""
+    from sparc_gym_amd.vec_env import xcd_local_puzzle_index
     gid = np.asarray(gid, dtype=np.uint64)
     if placement == "auto":
         placement = "xcd" if P > 1024 and P % 8 == 0 else "hash"
-    if placement == "hash" or P < 8:
+    if placement == "hash" or P < 8 or P % 8:
         return (gid * np.uint64(2654435761) % np.uint64(P)).astype(np.int64), "hash"
-    span = P // 8
-    slot = gid - gid[0] if len(gid) else gid
-    grp = (slot // np.uint64(256)) % np.uint64(8)
-    k = (slot // np.uint64(2048)) * np.uint64(256) + slot % np.uint64(256)   # the env's index in its XCD group
-    return (grp * np.uint64(span) + k * np.uint64(2654435761) % np.uint64(span)).astype(np.int64), "xcd"
+    off = int(gid[0]) if len(gid) else 0
+    return xcd_local_puzzle_index(len(gid), P, off), "xcd"
 
 
 def rule_rollout_kernel(proc, table):

@@ -8,7 +8,8 @@ include/sparc_gym_amd.h; there is no CPU fallback.
 from . import puzzles, synthetic  # noqa: F401
 from .puzzles import PuzzleTable, pack_table, process_puzzles  # noqa: F401
 
-__all__ = ["SPaRC_Gym", "SPaRCVecEnv", "process_puzzles", "pack_table", "PuzzleTable", "register"]
+__all__ = ["SPaRC_Gym", "SPaRCVecEnv", "xcd_local_puzzle_index", "process_puzzles", "pack_table", "PuzzleTable",
+           "register"]
 
 
 def __getattr__(name):
@@ -20,6 +21,9 @@ def __getattr__(name):
     if name == "SPaRCVecEnv":
         from .vec_env import SPaRCVecEnv
         return SPaRCVecEnv
+    if name == "xcd_local_puzzle_index":
+        from .vec_env import xcd_local_puzzle_index
+        return xcd_local_puzzle_index
     raise AttributeError(name)
 
 
