@@ -185,12 +185,15 @@ def cpu_procs(world, usable=None):
 
 
 def cpu_baseline_rules(proc, tb, max_steps, seconds, procs=0):
-    """The reference-speed full step() including its rule audit: oracle/cpu_ref.py's step core +
-    oracle/rules_ref.py's _validate_rules restatement TWICE per step, as the reference runs it
-    (SPaRC_Gym.py:1227 with the step's flags, and 1011 in _get_info with both False), pure
-    Python, 1 thread, random actions.  Next-step autoreset as the GPU kernel counts it: the step
-    after a done step is the reset (reset() -> _load_puzzle 182 and _get_info 1011: two audits),
-    one env-step.  The rate with one audit per step is reported beside it."""
+    """The reference's full step() including its rule audit, on the CPU: oracle/sparc_oracle.c's
+    step + oracle/sparc_rules_oracle.c's port of _validate_rules TWICE per step, as the reference
+    runs it (SPaRC_Gym.py:1227 with the step's flags, and 1011 in _get_info with both False), one
+    env per thread, counter-hash random actions (the C port, as every other config's baseline),
+    and beside it the pure-Python restatements (oracle/cpu_ref.py + oracle/rules_ref.py, the
+    reference's own speed).  Next-step autoreset as the GPU kernel counts it: the step after a
+    done step is the reset (reset() -> _load_puzzle 182 and _get_info 1011: two audits), one
+    env-step."""
+    from oracle import COracle, RulesCOracle
     from oracle.cpu_ref import CpuRefEnv
     from oracle import rules_ref
     pool = [{"x_size": p["x_size"], "y_size": p["y_size"], "start": list(p["start_location"]),
@@ -198,7 +201,16 @@ def cpu_baseline_rules(proc, tb, max_steps, seconds, procs=0):
              "solution_paths": p["solution_paths"], "gaps": p["obs_array"]["gaps"]} for p in proc]
     refp = [dict(p) for p in proc]
 
-    def run(audits, secs):
+    def run_c(secs):
+        o = COracle(pool, 1, tb, max_steps, autoreset=1)
+        o.reset([0])
+        ro = RulesCOracle(proc)
+        k, t1 = 0, time.perf_counter()
+        while time.perf_counter() - t1 < secs:
+            k += ro.rollout(o.pool, o.envs[0], 2000, seed=1, traceback=tb, max_steps=max_steps, audits=2)
+        return k, time.perf_counter() - t1
+
+    def run_py(audits, secs):
         rng = np.random.default_rng(0)
         q = 0
         env = CpuRefEnv(pool[q], tb, max_steps)
@@ -219,21 +231,29 @@ def cpu_baseline_rules(proc, tb, max_steps, seconds, procs=0):
             k += 1
         return k, time.perf_counter() - t1
 
-    k, dt = run(2, seconds)
-    k1, dt1 = run(1, min(seconds, 5.0))
-    out = {"value": round(k / dt, 1), "unit": "env-steps/s", "cores": 1, "kind": "port",
-           "sample": f"oracle/cpu_ref.py step() + oracle/rules_ref.py rule audit twice per step as the reference "
-                     f"(SPaRC_Gym.py:1227, 1011; pure Python, the reference's algorithms), 1 env, {k} steps incl. "
-                     f"next-step autoreset steps, random actions, {dt:.1f} s, 1 thread; CPU "
-                     f"{platform.processor() or platform.machine()}, os.cpu_count()={os.cpu_count()}",
-           "value_1core": round(k / dt, 1),
-           "value_1core_audit_once": round(k1 / dt1, 1)}
+    kc, dtc = run_c(min(seconds, 5.0))
+    k, dt = run_py(2, min(seconds, 5.0))
+    k1, dt1 = run_py(1, min(seconds, 3.0))
+    cpu = f"CPU {platform.processor() or platform.machine()}, os.cpu_count()={os.cpu_count()}"
+    out = {"value": round(kc / dtc, 1), "unit": "env-steps/s", "cores": 1, "kind": "port",
+           "sample": f"oracle/sparc_oracle.c step() + oracle/sparc_rules_oracle.c rule audit twice per step as the "
+                     f"reference (SPaRC_Gym.py:1227, 1011), 1 env, {kc} steps incl. next-step autoreset steps, "
+                     f"random actions, {dtc:.1f} s, 1 thread; {cpu}",
+           "value_1core": round(kc / dtc, 1),
+           "python_port_value": round(k / dt, 1),
+           "python_port_sample": f"oracle/cpu_ref.py step() + oracle/rules_ref.py audit twice per step (pure Python, "
+                                 f"the reference's algorithms), 1 env, {k} steps, {dt:.1f} s, 1 thread",
+           "python_port_value_audit_once": round(k1 / dt1, 1)}
     # the same on one process per core of this GPU's share of the host (BASELINE.md's plan)
-    mp_ = _cpu_bench_multi("c3r", "py_rules", max_steps, seconds, procs)
+    mc = _cpu_bench_multi("c3r", "c_rules", max_steps, seconds, procs)
+    if mc:
+        out.update(value=mc["value"], cores=mc["procs"],
+                   sample=out["sample"] + f"; value: {mc['procs']} processes x 1 env, {mc['seconds']:.0f} s "
+                                          f"(oracle/cpu_bench.py --impl c_rules, two audits per step)")
+    mp_ = _cpu_bench_multi("c3r", "py_rules", max_steps, min(seconds, 5.0), procs)
     if mp_:
-        out.update(value=mp_["value"], cores=mp_["procs"],
-                   sample=out["sample"] + f"; value: {mp_['procs']} processes x 1 env, {mp_['seconds']:.0f} s "
-                                          f"(oracle/cpu_bench.py --impl py_rules, two audits per step)")
+        out["python_port_multicore"] = {"value": mp_["value"], "procs": mp_["procs"],
+                                        "sample": "oracle/cpu_bench.py --impl py_rules, two audits per step"}
     return out
 
 

@@ -11,6 +11,8 @@ bench.py) with counter-based random actions and next-step autoreset, for `second
 --obs it also writes the visited / agent_location planes of every step (config c4).  Prints
 one JSON line: {"value": env-steps/s summed over processes, "procs": P, ...}.
 
+--impl c_rules runs one env per process through sparc_oracle.c's step plus the C port of the rule
+audit (sparc_rules_oracle.c) twice per step: the c3r baseline at C speed.
 --impl py runs the pure-Python restatement instead (oracle/cpu_ref.py: the reference's step()
 core at reference speed, one env at a time), --impl py_rules the same plus the rule audit of
 oracle/rules_ref.py twice per step, as the reference's full step() runs _validate_rules (941-950) at
@@ -76,6 +78,25 @@ def _worker(args):
     return n * steps, time.perf_counter() - t0
 
 
+def _worker_c_rules(args):
+    """One env through oracle/sparc_rules_oracle.c's oracle_rules_rollout: sparc_oracle.c's step
+    plus the C port of the rule audit twice per step (SPaRC_Gym.py:1227 and 1011), next-step
+    autoreset onto the next puzzle (the reset step audits twice too: 182, 1011), counter-hash
+    random actions."""
+    proc, tb, max_steps, seconds, rank = args
+    from oracle import COracle, RulesCOracle
+    pool = [{"x_size": p["x_size"], "y_size": p["y_size"], "start": list(p["start_location"]),
+             "target": list(p["target_location"]), "solution_count": p["solution_count"],
+             "solution_paths": p["solution_paths"], "gaps": p["obs_array"]["gaps"]} for p in proc]
+    o = COracle(pool, 1, tb, max_steps, autoreset=1)
+    o.reset([(rank * 2654435761) % len(pool)])
+    ro = RulesCOracle(proc)
+    k, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        k += ro.rollout(o.pool, o.envs[0], 2000, seed=1 + rank, traceback=tb, max_steps=max_steps, audits=2)
+    return k, time.perf_counter() - t0
+
+
 def _worker_py(args):
     """One env at a time through oracle/cpu_ref.py (+ oracle/rules_ref.py's audit twice per step,
     SPaRC_Gym.py:1227 and 1011).  Next-step autoreset counted as the GPU kernel and the C oracle
@@ -116,7 +137,7 @@ def main():
     ap.add_argument("--puzzles", type=int, default=1024)
     ap.add_argument("--max-steps", type=int, default=2000)
     ap.add_argument("--obs", type=int, nargs=2, default=None, metavar=("X", "Y"))
-    ap.add_argument("--impl", default="c", choices=["c", "py", "py_rules"])
+    ap.add_argument("--impl", default="c", choices=["c", "py", "py_rules", "c_rules"])
     a = ap.parse_args()
     usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     procs = a.procs if a.procs > 0 else max(1, min(16, usable))
@@ -127,6 +148,12 @@ def main():
         build()                                                  # compile once, before forking
         with mp.get_context("fork").Pool(procs) as p:
             res = p.map(_worker, [(pool, tb, a.max_steps, a.seconds, a.obs, r) for r in range(procs)])
+    elif a.impl == "c_rules":
+        proc = make_proc(a.config, a.puzzles)
+        from oracle import build
+        build()
+        with mp.get_context("fork").Pool(procs) as p:
+            res = p.map(_worker_c_rules, [(proc, tb, a.max_steps, a.seconds, r) for r in range(procs)])
     else:
         proc = make_proc(a.config, a.puzzles)
         with mp.get_context("fork").Pool(procs) as p:
