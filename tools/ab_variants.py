@@ -56,6 +56,8 @@ VARIANTS = {
     "funi": [("sparc_rules.hpp", '            while (true) {\n                const uint64_t r1 = dilate_w1(r0, aw, P);\n                if (r1 == r0) break;\n                r0 = dilate_w1(r1, aw, P);\n                if (r0 == r1) break;\n            }', '            while (true) {   // a wave-uniform exit: converged lanes dilate on unchanged (idempotent)\n                const uint64_t r1 = dilate_w1(r0, aw, P);\n                const uint64_t r2 = dilate_w1(r1, aw, P);\n                const bool ch = r2 != r1;\n                r0 = r2;\n                if (!__any(ch)) break;\n            }')],
     # the move wave's pop test and back-position select without VCC (a shift and two v_bfi)
     "valusel": [("sparc_move1.hpp", '        if constexpr (TB) pop = pos == rp ? bias : 0u;                              // 1141-1166', '        if constexpr (TB) pop = bias >> (pos ^ rp);   // pos == rp ? bias : 0 (both < 32): no VCC   1141-1166'), ("sparc_move1.hpp", '            rp = fwd ? arp : (pop ? pnr : rp);', '            uint32_t r1;   // rp = fwd ? arp : (pop ? pnr : rp) by two v_bfi (fwd, pop in {0, 1})\n            asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r1) : "v"(0u - pop), "v"(pnr), "v"(rp));\n            asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(rp) : "v"(0u - fwd), "v"(arp), "v"(r1));')],
+    # W = 1 rule rows loaded in the order the audit uses them (regions first, path planes last)
+    "roworder": [("sparc_rules.hpp", '#pragma unroll\n    for (int k = 0; k < 10; ++k) r.pl[k] = BB<W>::load(g + k * W);\n    const uint64_t m0 = g[10 * W], m1 = g[10 * W + 1];', '    uint64_t m0, m1;\n    if constexpr (W == 1) {\n        // what the regions need first (cells, lattice, gaps: bytes 0-23; the meta words 80-95),\n        // then the path-rule planes (24-63), so the flood waits for the first three loads only\n        const ulonglong2* g2 = reinterpret_cast<const ulonglong2*>(g);\n        const ulonglong2 a = g2[0], b = g2[1], m = g2[5];\n        __asm__ volatile("" ::: "memory");\n        const ulonglong2 c = g2[2], d = g2[3];\n        r.pl[0].w[0] = a.x; r.pl[1].w[0] = a.y; r.pl[2].w[0] = b.x; r.pl[3].w[0] = b.y;\n        r.pl[4].w[0] = c.x; r.pl[5].w[0] = c.y; r.pl[6].w[0] = d.x; r.pl[7].w[0] = d.y;\n        r.pl[8].w[0] = 0; r.pl[9].w[0] = 0;   // NOTFIRST / NOTLAST: the W > 1 flood only\n        m0 = m.x;\n        m1 = m.y;\n    } else {\n#pragma unroll\n        for (int k = 0; k < 10; ++k) r.pl[k] = BB<W>::load(g + k * W);\n        m0 = g[10 * W];\n        m1 = g[10 * W + 1];\n    }')],
     # the path rules' triangle count by v_bitop3 (audit_path)
     "tribitop": [("sparc_rules.hpp", '    // triangles: bit-sliced count of path neighbours (x±1: ±P, y±1: ±1)\n    const BB<W> a = vis.shr(P), b = vis.shl(P), c = vis.shr(1), d = vis.shl(1);\n    const BB<W> s1 = a ^ b, c1 = a & b, s2 = c ^ d, c2 = c & d;\n    const BB<W> n0 = s1 ^ s2, k0 = s1 & s2, n1 = c1 ^ c2 ^ k0, n2 = c1 & c2;\n    const BB<W> bad = pr.pl[kB_TRI] & ((n0 ^ pr.pl[kB_TRI0]) | (n1 ^ pr.pl[kB_TRI1]) | (n2 ^ pr.pl[kB_TRI2]));\n    const bool tri_ok = !bad.any();', '    // triangles: bit-sliced count of path neighbours (x±1: ±P, y±1: ±1) per 32-bit half, a full\n    // adder of a, b, c (sum s, carry M) plus d: bit 0 s ^ d, bit 1 M ^ (s & d), bit 2 M & s & d,\n    // each compared with the planes by v_bitop3 (7 per half against 13 plain logic VALU)\n    const BB<W> a = vis.shr(P), b = vis.shl(P), c = vis.shr(1), d = vis.shl(1);\n    uint32_t bad = 0;\n#pragma unroll\n    for (int h = 0; h < 2 * W; ++h) {\n        auto half = [h](const BB<W>& x) { return (uint32_t)(x.w[h >> 1] >> (32 * (h & 1))); };\n        const uint32_t ah = half(a), bh = half(b), ch = half(c), dh = half(d);\n        const uint32_t s = bitop3<0x96>(ah, bh, ch);                     // a ^ b ^ c\n        const uint32_t M = bitop3<0xE8>(ah, bh, ch);                     // majority (the carry)\n        const uint32_t e0 = bitop3<0x96>(s, dh, half(pr.pl[kB_TRI0]));   // count bit 0 ^ TRI0\n        const uint32_t n1 = bitop3<0x78>(M, s, dh);                      // M ^ (s & d)\n        const uint32_t n2 = bitop3<0x80>(M, s, dh);                      // M & s & d\n        const uint32_t f = bitop3<0xF6>(e0, n1, half(pr.pl[kB_TRI1]));   // e0 | (n1 ^ TRI1)\n        const uint32_t g = bitop3<0xF6>(f, n2, half(pr.pl[kB_TRI2]));    // f | (n2 ^ TRI2)\n        bad |= g & half(pr.pl[kB_TRI]);\n    }\n    const bool tri_ok = bad == 0u;'), ("sparc_rules.hpp", 'template <int W>\n__device__ __forceinline__ uint32_t audit_path(', '// v_bitop3_b32 d = TT[x << 2 | y << 1 | z] bitwise (gfx950)\ntemplate <uint32_t TT>\n__device__ __forceinline__ uint32_t bitop3(uint32_t x, uint32_t y, uint32_t z) {\n    uint32_t d;\n    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4" : "=v"(d) : "v"(x), "v"(y), "v"(z), "i"(TT));\n    return d;\n}\n\ntemplate <int W>\n__device__ __forceinline__ uint32_t audit_path(')],
     # the plane writer's piece loop unrolled twice (more stores in flight per wave)
