@@ -344,10 +344,10 @@ int sparc_set_rule_limits(void *ctx, uint32_t fit_cap_nodes, uint64_t table_entr
  *                                      without the I/O-wave codes); 0: default
  *  SPARC_VARIANT_RULE_ROLLOUT_GENERIC  1: rule rollouts on the generic per-wave rule kernel even
  *                                      where k_rollout1r applies; 0: default
- *  SPARC_VARIANT_R1R_SHAPE             k_rollout1r's <G, A, RT>: 0 <2, 5, 10> (default),
- *                                      1 <4, 3, 12>, 2 <2, 4, 12>; incremental audits (each
- *                                      audit wave keeps its envs' regions from step to step):
- *                                      3 <4, 1, 4>, 4 <2, 3, 15>
+ *  SPARC_VARIANT_R1R_SHAPE             k_rollout1r's <G, A, RT>: 0 <2, 5, 15> (default),
+ *                                      1 <4, 3, 12>, 2 <2, 4, 12>, 5 <2, 5, 10>; incremental
+ *                                      audits (each audit wave keeps its envs' regions from
+ *                                      step to step): 3 <4, 1, 4>, 4 <2, 3, 15>
  *  SPARC_VARIANT_OBS_INLINE            1: sparc_rollout_obs_device on the per-wave kernel that
  *                                      writes its own planes; 0: default (writer waves)
  *  SPARC_VARIANT_MIXED_TRIE            W = 1 pools past the LDS row budget: the split kernel on

@@ -1987,7 +1987,7 @@ struct Ctx {
     // kernel variants with identical results, set only by sparc_set_variant (A/B runs, tests)
     bool rules_generic = false;   // rule rollouts on k_rollout<..., RULES>
     bool io_codes_off = false;    // k_rollout1s / k_rolloutWs keep the reward codes on the trie wave
-    int r1r_shape = 0;            // k_rollout1r's <G, A, RT> (0: <2, 5, 10>; 1-4: A/B, tests)
+    int r1r_shape = 0;            // k_rollout1r's <G, A, RT> (0: <2, 5, 15>; 1-5: A/B, tests)
     bool obs_inline = false;      // 'new'-plane rollouts on k_rollout<..., OBS> instead of k_rollout_obsw
     // exact-fit searches past the GPU's node cap (sparc_set_fit_cap) are finished on the host
     // from these copies of the rule table (sparc_rules.hpp exact_fit, the same code)
@@ -2874,7 +2874,10 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
             using GG = R1Geom<G, A, RT>;
             const size_t blocks = (c->n + GG::kEnvs - 1) / GG::kEnvs;
             const size_t tbytes = table_lds_bytes<1>(c->num_puzzles);
-            const bool lds_table = GG::kBase + tbytes <= kMaxDynLds;
+            // the puzzle rows go to LDS only while a 12-wave workgroup still leaves room for a
+            // second one on the CU (80 KB each); past that the step waves read them from the L2
+            // (their resets have slack: the audit waves set the pace)
+            const bool lds_table = GG::kBase + tbytes <= (GG::kBlock <= 768 ? (size_t)80 * 1024 : kMaxDynLds);
             const size_t shm = GG::kBase + (lds_table ? tbytes : 0);
             auto launch = [&](auto kern, const uint8_t* a) {
                 if (shm > 64 * 1024 && (lds_rc = allow_big_lds(c, reinterpret_cast<const void*>(kern)))) return;
@@ -2894,8 +2897,11 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
             if (c->cfg.traceback) go(std::true_type{});
             else go(std::false_type{});
         };
-        // <2, 5, 10>: 128 envs, 2 step + 10 audit waves per workgroup, two workgroups per CU (six
-        // waves per SIMD at 66-80 VGPRs); MI355X, c3r, 50-step launches at 65,536 envs: 0.1245 ms
+        // <2, 5, 15>: 128 envs, 2 step + 10 audit waves per workgroup, two workgroups per CU (six
+        // waves per SIMD at 66-80 VGPRs), three jobs per audit lane and 15-step tile (the waves'
+        // skew at the tile barrier averages over more jobs), the puzzle rows from the L2 (76 KB of
+        // rings per workgroup); MI355X, c3r 2,000-step launches: 2.51 ms against 2.60 for
+        // <2, 5, 10> (profiles/r06/ab_c3r_flood).  Round 4, 50-step launches: <2, 5, 10> 0.1245 ms
         // against 0.1338 for <4, 3, 12> (one 16-wave workgroup per CU, its LDS) and 0.1275 for
         // <2, 4, 12> (profiles/r04/ab_run2)
         switch (c->r1r_shape) {
@@ -2906,7 +2912,8 @@ int rollout_impl(Ctx* c, int32_t T, const uint8_t* d_act, uint64_t seed, uint64_
             // (<2, 1, 8> 9.2, <2, 2, 16> 7.8; profiles/r06/ab_c3r_inc)
             case 3: go_shape(R1Shape<4, 1, 4, true, 4>{}); break;
             case 4: go_shape(R1Shape<2, 3, 15, true, 4>{}); break;
-            default: go_shape(R1Shape<2, 5, 10>{}); break;
+            case 5: go_shape(R1Shape<2, 5, 10>{}); break;
+            default: go_shape(R1Shape<2, 5, 15>{}); break;
         }
         if (lds_rc) return lds_rc;
         return launch_check(c);
@@ -3561,7 +3568,7 @@ int sparc_set_variant(void* ctx, int32_t which, int32_t value) {
             c->rules_generic = value == 1;
             return SPARC_OK;
         case SPARC_VARIANT_R1R_SHAPE:
-            if (value < 0 || value > 4) break;
+            if (value < 0 || value > 5) break;
             c->r1r_shape = value;
             return SPARC_OK;
         case SPARC_VARIANT_OBS_INLINE:

@@ -396,11 +396,12 @@ def test_rules_table_budget_cutoff_mixed_pool(on_gpu, generic, budget):
     assert len(np.unique(bits)) > 4
 
 
-@pytest.mark.parametrize("shape", [1, 2, 3, 4])
+@pytest.mark.parametrize("shape", [1, 2, 3, 4, 5])
 def test_rule_rollout_shapes_equal_default(on_gpu, shape):
     """Every compiled shape of the W = 1 rule rollout (sparc_set_variant SPARC_VARIANT_R1R_SHAPE: k_rollout1r <G, A, RT> =
-    <4, 3, 12> and <2, 4, 12>, and the incremental audits 3, 4 (RegionSet1: regions kept from step
-    to step, re-flooded only where a step splits one) besides the default <2, 5, 10>) gives the same
+    <4, 3, 12>, <2, 4, 12> and <2, 5, 10> (the round-6 default before 15-step tiles), and the
+    incremental audits 3, 4 (RegionSet1: regions kept from step to step, re-flooded only where a
+    step splits one) besides the default <2, 5, 15>) gives the same
     reward codes, flags, stats, rule bits and final state as the default shape (oracle-pinned by
     test_rollout_rules_c3r_full_size), over two launches (the second with a partial last tile) on
     a ragged batch (a partial last group)."""
